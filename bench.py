@@ -1,0 +1,216 @@
+#!/usr/bin/env python3
+"""bench.py — CpG-island HMM hot path on MI355X: train + Viterbi bases/s.
+
+Metric (BASELINE.json): bases/sec train+Viterbi at 1/2/4/8 MI355X; % HBM peak; CPU ref bases/s.
+Workload (configs[1]): 46 Mbp chr21-sized synthetic sequence per GPU.  One step =
+  train  : Baum-Welch E-step (expected counts, 65,536-base chunks, :130-141/:200)
+           + labelled int64 counts (truth labels) + the reducer's cross-GPU merge
+           (int64 all-reduce, fp64 all-gather + fixed-order sum over RCCL)
+  decode : exact Viterbi of every whole 1,048,576-base chunk (:256-260)
+           + island scan/filter (:262-339)
+over bases already resident in HBM.  Weak scaling: rank r owns its own contiguous,
+1 Mi-aligned 46 Mbp shard of the genome; value = bases of all ranks / step time (max over
+ranks).  Launched as `python bench.py` (N=1) or via torch.distributed.run for N>1.
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "bases/sec train+Viterbi at 1/2/4/8 MI355X; % HBM peak; CPU ref bases/s"
+SEED = 20251015 + 1            # seed + config index
+N_PER_GPU = 46_000_000         # configs[1]: 46 Mbp chr21-sized
+SHARD_STRIDE = 44 << 20        # 1 Mi-aligned shard starts (44 decode chunks >= 46e6 bases)
+TRAIN = 65536
+DECODE = 1 << 20
+HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+# algorithmic bytes per base of each phase
+BYTES_PER_BASE = {"estep": 0.25, "counts": 0.375, "viterbi": 0.375, "islands": 0.375}
+
+
+def log(*a):
+    print(*a, file=sys.stderr, flush=True)
+
+
+def cpu_baseline(seed, sample_bases):
+    """The oracle (C restatement of the reference, Mahout-order 8-state Viterbi with
+    Math.log in the inner loop, textbook E-step, counts, island scan) on 1 host core over a
+    bounded sample of the same workload."""
+    from cpgisland_amd import device as D
+    from oracle import coracle as co
+    from oracle import pyref as pr
+    packed, sign = D.synth_host(seed, 0, sample_bases)
+    obs = pr.unpack(packed, sample_bases)
+    truth = pr.unpack_bits(sign, sample_bases)
+    m = co.initial_model()
+    t0 = time.perf_counter()
+    co.estep(m, obs, TRAIN)
+    co.count_labelled(obs, truth, TRAIN)
+    co.decode_chunks(m, obs, DECODE)
+    dt = time.perf_counter() - t0
+    return {"value": sample_bases / dt, "unit": "bases/s", "cores": 1, "kind": "port",
+            "sample": f"{sample_bases} bases ({sample_bases // DECODE} decode chunks, "
+                      f"{sample_bases // TRAIN} train chunks) of the same synthetic genome; "
+                      f"oracle/cpg_oracle.c single-threaded, {dt:.1f} s",
+            "seconds": dt}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--bases", type=int, default=N_PER_GPU, help="bases per GPU")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-sample", type=int, default=8 * DECODE)
+    ap.add_argument("--flush-mb", type=int, default=0,
+                    help="write this many MiB of scratch between steps (cold Infinity Cache)")
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    dist = world > 1
+    if dist:
+        os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+        torch.cuda.set_device(local)
+        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+    dev = torch.device("cuda", local)
+    torch.cuda.set_device(dev)
+
+    from cpgisland_amd import Context, HmmModel
+    from cpgisland_amd import device as D
+
+    N = args.bases
+    start = rank * SHARD_STRIDE if N <= SHARD_STRIDE else rank * ((N + DECODE - 1) // DECODE * DECODE)
+    log(f"[rank {rank}] synthesising {N} bases at offset {start}")
+    packed, sign = D.synth_host(SEED, start, N)
+    dp = D.to_device(packed, dev)
+    ds = D.to_device(sign, dev)
+    ctx = Context(local)
+    ctx.reserve(N)
+    model0 = HmmModel.initial()
+    ndec = N // DECODE
+    first_chunk = start // DECODE
+    so = torch.empty(D.words32(N) + 4, dtype=torch.int32, device=dev)
+    score = torch.empty(max(ndec, 1), dtype=torch.float64, device=dev)
+    ecnt = torch.empty(105, dtype=torch.float64, device=dev)
+    lcnt = torch.empty(124, dtype=torch.int64, device=dev)
+    icap = 1 << 20
+    iout = torch.empty((icap, 32), dtype=torch.uint8, device=dev)
+    icnt = torch.zeros(1, dtype=torch.int64, device=dev)
+    gath = torch.empty((world, 105), dtype=torch.float64, device=dev) if dist else None
+    flush = torch.empty(args.flush_mb << 18, dtype=torch.float32, device=dev) if args.flush_mb else None
+
+    # trained model for the decode: one Baum-Welch iteration from the reference's model
+    D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
+    c = ecnt.cpu().numpy()
+    if dist:
+        allc = [torch.empty_like(ecnt) for _ in range(world)]
+        torch.distributed.all_gather(allc, ecnt)
+        c = np.sum([x.cpu().numpy() for x in allc], axis=0)
+    from cpgisland_amd import baumwelch
+    model1 = baumwelch.normalize(c)
+
+    ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+          for k in ("estep", "counts", "reduce", "viterbi", "islands")}
+    acc = {k: 0.0 for k in ev}
+
+    def step(timed):
+        def mark(k, i):
+            if timed:
+                ev[k][i].record()
+        mark("estep", 0)
+        D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
+        mark("estep", 1)
+        mark("counts", 0)
+        D.count_labelled(ctx, dp, ds, N, TRAIN, out=lcnt)
+        mark("counts", 1)
+        mark("reduce", 0)
+        if dist:   # the reducer: int64 sums are exact in any order; fp64 in rank order
+            torch.distributed.all_reduce(lcnt)
+            torch.distributed.all_gather_into_tensor(gath, ecnt)
+            ecnt.copy_(gath.sum(dim=0))
+        mark("reduce", 1)
+        mark("viterbi", 0)
+        D.viterbi(ctx, model1, dp, N, DECODE, sign_out=so, score=score)
+        mark("viterbi", 1)
+        mark("islands", 0)
+        D.islands(ctx, dp, so, N, DECODE, cap=icap, first_chunk=first_chunk, out=iout, count=icnt)
+        mark("islands", 1)
+
+    for _ in range(args.warmup):
+        step(False)
+        if flush is not None:
+            flush.fill_(1.0)
+    torch.cuda.synchronize()
+    ctx.sync(None)
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        if flush is not None:
+            flush.fill_(1.0)
+        step(True)
+        torch.cuda.synchronize()
+        for k, (a, b) in ev.items():
+            acc[k] += a.elapsed_time(b)
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ctx.sync(None)     # raises if any kernel self-check (exactness) failed
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    steps = args.steps
+    ms_per_step = elapsed * 1e3 / steps
+    value = N * world * steps / elapsed
+    phases = {k: v / steps for k, v in acc.items()}
+    if flush is not None:
+        phases_total = sum(phases.values())
+        ms_per_step = phases_total   # exclude the cache-flush writes from the step time
+        value = N * world / (phases_total / 1e3)
+
+    if rank == 0:
+        dom = max(("estep", "counts", "viterbi", "islands"), key=lambda k: phases[k])
+        ach = BYTES_PER_BASE[dom] * N / (phases[dom] / 1e3) / 1e9
+        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
+                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "bytes_per_base": BYTES_PER_BASE[dom],
+                "note": "phase time from HIP events on the launch stream; see DESIGN.md for "
+                        "the VALU bound of the fp64 phases"}
+        out = {"metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
+               "steps": steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+               "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+               "dtype": "f64", "data": "synthetic (counter-based planted-island genome, "
+                                        f"seed {SEED})",
+               "config": {"workload": "C2: 46 Mbp chr21-sized per GPU; BW E-step + labelled "
+                                      "counts + RCCL reduce + exact Viterbi + islands",
+                          "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
+                          "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
+                          "islands_found": int(icnt.item())},
+               "phases_ms": {k: round(v, 4) for k, v in phases.items()},
+               "roofline": roof}
+        if not args.no_cpu_baseline and world == 1:
+            out["cpu_baseline"] = cpu_baseline(SEED, args.cpu_sample)
+        else:
+            out["cpu_baseline"] = None
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,78 @@
+"""Baum-Welch training — the host side of BaumWelchDriver.runBaumWelchMR (called at
+/root/reference/CpGIslandFinder.java:200-201; MAHOUT-627 MapReduce classes, unvendored).
+
+  mapper   -> estep()      the fp64 expected-count stripes of every 65,536-base chunk
+                           (GPU kernel, cpg_bw_estep_d)
+  reducer  -> normalize()  sum of stripes + row normalisation (cpg_bw_normalize)
+  driver   -> run()        iterate until converged or max_iter (convergence rule:
+                           Mahout HmmTrainer's — the MAHOUT-627 rule is unpinned)
+Multi-GPU: each rank runs the mapper on its shard; the stripes are all-gathered and summed
+in rank order (deterministic), then every rank normalises identically (no broadcast).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+from . import _lib
+from ._lib import check, lib, ptr
+from .hmm import Context, HmmModel
+
+
+def normalize(counts) -> HmmModel:
+    """The reducer: counts (cpg_counts_f64 layout, 105 doubles) -> row-normalised model."""
+    c = np.ascontiguousarray(counts, dtype=np.float64)
+    assert c.size == _lib.COUNTS_F64_N
+    m = np.zeros(_lib.MODEL_N, np.float64)
+    check(lib.cpg_bw_normalize(ptr(c), ptr(m)))
+    return HmmModel.from_struct(m)
+
+
+def normalize_labelled(counts) -> HmmModel:
+    """M-step of the labelled (hard-label) counts, cpg_counts_i64 layout."""
+    c = np.ascontiguousarray(counts, dtype=np.int64)
+    m = np.zeros(_lib.MODEL_N, np.float64)
+    check(lib.cpg_counts_normalize(ptr(c), ptr(m)))
+    return HmmModel.from_struct(m)
+
+
+def converged(old: HmmModel, new: HmmModel, epsilon: float) -> bool:
+    """Mahout HmmTrainer.checkConvergence: sqrt(sum (dA)^2) + sqrt(sum (dB)^2) < eps."""
+    na = math.sqrt(float(np.sum((old.a - new.a) ** 2)))
+    nb = math.sqrt(float(np.sum((old.b - new.b) ** 2)))
+    return na + nb < epsilon
+
+
+def estep(ctx: Context, model: HmmModel, packed, nbases: int,
+          chunk_len: int = _lib.TRAIN_CHUNK, allgather=None):
+    """The mapper over one shard (device tensor) -> host counts (105 doubles).  With
+    `allgather` (torch.distributed), stripes of all ranks are summed in rank order."""
+    import torch
+    from . import device as D
+    out = D.bw_estep(ctx, model, packed, nbases, chunk_len)
+    if allgather is not None:
+        ws = allgather.get_world_size()
+        buf = torch.empty((ws, out.numel()), dtype=out.dtype, device=out.device)
+        allgather.all_gather_into_tensor(buf, out)
+        return buf.cpu().numpy().sum(axis=0)
+    return out.cpu().numpy()
+
+
+def run(ctx: Context, packed, nbases: int, model: HmmModel | None = None,
+        convergence: float = 0.005, max_iter: int = 10,
+        chunk_len: int = _lib.TRAIN_CHUNK, allgather=None):
+    """runBaumWelchMR(conf, input, modelIn, output, ..., convergence, "rescaling", numIter).
+    Returns (trained model, iterations run, log-likelihood of the last E-step)."""
+    model = model or HmmModel.initial()
+    ll = -math.inf
+    it = 0
+    for it in range(1, max_iter + 1):
+        counts = estep(ctx, model, packed, nbases, chunk_len, allgather)
+        ll = float(counts[-1])
+        new = normalize(counts)
+        done = converged(model, new, convergence)
+        model = new
+        if done:
+            break
+    return model, it, ll

@@ -1,0 +1,381 @@
+// cpg_api.cpp — the C-ABI of libcpg.so (include/cpg.h): context, device workspace,
+// the HBM-resident "_d" entry points and the host-buffer wrappers that mirror the
+// reference call sites (CpGIslandFinder.java:200 training, :260 decode, :262-339 islands).
+
+#include <cmath>
+#include <cstring>
+#include <vector>
+
+#include "cpg_internal.h"
+
+namespace cpg {
+
+int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
+    Buf& b = ctx->ws[slot];
+    if (b.bytes < bytes) {
+        if (b.p) {
+            CPG_HIP(hipStreamSynchronize(ctx->stream));
+            CPG_HIP(hipFree(b.p));
+            b.p = nullptr;
+            b.bytes = 0;
+        }
+        size_t sz = bytes + bytes / 8 + 4096;
+        CPG_HIP(hipMalloc(&b.p, sz));
+        b.bytes = sz;
+    }
+    *out = b.p;
+    return CPG_OK;
+}
+
+int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
+    Buf& b = ctx->pin[slot];
+    if (b.bytes < bytes) {
+        if (b.p) {
+            CPG_HIP(hipStreamSynchronize(ctx->stream));
+            CPG_HIP(hipHostFree(b.p));
+            b.p = nullptr;
+            b.bytes = 0;
+        }
+        CPG_HIP(hipHostMalloc(&b.p, bytes, hipHostMallocDefault));
+        b.bytes = bytes;
+    }
+    *out = b.p;
+    return CPG_OK;
+}
+
+namespace {
+
+enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
+       WS_OUT1 = 7, WS_OUT2 = 8 };
+
+// NULL is the HIP null stream (torch's default stream handle is 0 too); the host-buffer
+// wrappers pass the context's own stream explicitly
+hipStream_t pick(cpg_ctx*, void* stream) { return static_cast<hipStream_t>(stream); }
+
+bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
+
+// device copy of the per-binade tables of one model (model-only; cached per context)
+int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitTables** out) {
+    for (int i = 0; i < ctx->vtn; ++i)
+        if (std::memcmp(&ctx->vtc[i].model, m, sizeof *m) == 0) {
+            *out = ctx->vtc[i].d;
+            return CPG_OK;
+        }
+    cpg_ctx::VtSlot* sl;
+    if (ctx->vtn < cpg_ctx::kVtSlots) {
+        sl = &ctx->vtc[ctx->vtn++];
+        CPG_HIP(hipMalloc(&sl->d, sizeof(VitTables)));
+    } else {
+        sl = &ctx->vtc[ctx->vtnext];
+        ctx->vtnext = (ctx->vtnext + 1) % cpg_ctx::kVtSlots;
+        CPG_HIP(hipDeviceSynchronize());   // the evicted slot may still be read
+    }
+    sl->model = *m;
+    CPG_HIP(hipMemcpy(sl->d, &vt, sizeof(VitTables), hipMemcpyHostToDevice));
+    *out = sl->d;
+    return CPG_OK;
+}
+
+int check_layout(const void* packed, int64_t nbases, int64_t chunk_len) {
+    if (!packed && nbases > 0) return set_error(CPG_E_INVALID, "null packed buffer");
+    if (nbases < 0 || chunk_len <= 0)
+        return set_error(CPG_E_INVALID, "nbases=%lld chunk_len=%lld", (long long)nbases,
+                         (long long)chunk_len);
+    if (!aligned16(packed)) return set_error(CPG_E_INVALID, "packed buffer not 16-byte aligned");
+    return CPG_OK;
+}
+
+}  // namespace
+}  // namespace cpg
+
+using namespace cpg;
+
+extern "C" {
+
+int cpg_open(int device, cpg_ctx** out) {
+    if (!out) return set_error(CPG_E_INVALID, "null out");
+    *out = nullptr;
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess || n <= 0)
+        return set_error(CPG_E_DEVICE, "no HIP device available (%s)", hipGetErrorString(e));
+    if (device < 0 || device >= n) return set_error(CPG_E_INVALID, "device %d of %d", device, n);
+    CPG_HIP(hipSetDevice(device));
+    cpg_ctx* ctx = new cpg_ctx();
+    ctx->device = device;
+    CPG_HIP(hipStreamCreateWithFlags(&ctx->stream, hipStreamNonBlocking));
+    CPG_HIP(hipMalloc(&ctx->d_status, 256));
+    CPG_HIP(hipMemset(ctx->d_status, 0, 256));
+    *out = ctx;
+    return CPG_OK;
+}
+
+void cpg_close(cpg_ctx* ctx) {
+    if (!ctx) return;
+    (void)hipSetDevice(ctx->device);
+    (void)hipStreamSynchronize(ctx->stream);
+    for (auto& b : ctx->ws)
+        if (b.p) (void)hipFree(b.p);
+    for (auto& b : ctx->pin)
+        if (b.p) (void)hipHostFree(b.p);
+    if (ctx->d_status) (void)hipFree(ctx->d_status);
+    for (int i = 0; i < ctx->vtn; ++i) (void)hipFree(ctx->vtc[i].d);
+    (void)hipStreamDestroy(ctx->stream);
+    delete ctx;
+}
+
+int cpg_reserve(cpg_ctx* ctx, int64_t nbases) {
+    if (!ctx || nbases < 0) return set_error(CPG_E_INVALID, "bad argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    void* p;
+    int rc;
+    const int64_t nd = nbases / CPG_DECODE_CHUNK + 1, nt = nbases / CPG_TRAIN_CHUNK + 1;
+    if ((rc = ws_get(ctx, WS_COUNT, count_ws_bytes(nt), &p))) return rc;
+    if ((rc = ws_get(ctx, WS_VIT, viterbi_ws_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
+    if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
+    if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nt, CPG_TRAIN_CHUNK), &p))) return rc;
+    return CPG_OK;
+}
+
+int cpg_sync(cpg_ctx* ctx, void* stream) {
+    if (!ctx) return set_error(CPG_E_INVALID, "null ctx");
+    CPG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = pick(ctx, stream);
+    uint32_t st = 0;
+    CPG_HIP(hipMemcpyAsync(&st, ctx->d_status, 4, hipMemcpyDeviceToHost, s));
+    CPG_HIP(hipStreamSynchronize(s));
+    if (st) {
+        CPG_HIP(hipMemsetAsync(ctx->d_status, 0, 4, s));
+        CPG_HIP(hipStreamSynchronize(s));
+        return set_error(CPG_E_VERIFY,
+                         "kernel self-check failed (status 0x%x: %s%s%s)", st,
+                         (st & ST_VERIFY_ENTRY) ? "viterbi block exit != next entry; " : "",
+                         (st & ST_VERIFY_MAG) ? "composite out of exact range; " : "",
+                         (st & ST_VERIFY_CHAIN) ? "traceback chain mismatch" : "");
+    }
+    return CPG_OK;
+}
+
+// ---- device entry points ----------------------------------------------------------
+int cpg_count_labelled_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
+                         int64_t nbases, int64_t chunk_len, int64_t* d_counts, void* stream) {
+    if (!ctx || !d_counts) return set_error(CPG_E_INVALID, "null argument");
+    int rc = check_layout(d_packed, nbases, chunk_len);
+    if (rc) return rc;
+    if (chunk_len % 256) return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 256");
+    if (!aligned16(d_sign)) return set_error(CPG_E_INVALID, "sign buffer not 16-byte aligned");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    const int64_t nch = nbases / chunk_len;
+    void* ws;
+    if ((rc = ws_get(ctx, WS_COUNT, count_ws_bytes(nch), &ws))) return rc;
+    CPG_HIP(launch_count(d_packed, d_sign, nch, chunk_len, (uint64_t*)ws, d_counts,
+                         pick(ctx, stream)));
+    return CPG_OK;
+}
+
+int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                  int64_t nbases, int64_t chunk_len, uint32_t* d_sign_out, double* d_score,
+                  void* stream) {
+    if (!ctx || !model || !d_sign_out) return set_error(CPG_E_INVALID, "null argument");
+    int rc = check_layout(d_packed, nbases, chunk_len);
+    if (rc) return rc;
+    const int64_t nch = nbases / chunk_len;
+    if (nch > 1 && chunk_len % 256)
+        return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 256 for >1 chunk");
+    if (!aligned16(d_sign_out)) return set_error(CPG_E_INVALID, "sign_out not 16-byte aligned");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = pick(ctx, stream);
+    // undecoded tail -> '-' bits (whole words past the last chunk)
+    const int64_t w_done = (nch * chunk_len + 31) / 32, w_all = (nbases + 31) / 32;
+    if (w_all > w_done)
+        CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)(w_all - w_done) * 4, s));
+    if (nch == 0) return CPG_OK;
+    VitConsts vc;
+    static thread_local VitTables vt;
+    if ((rc = vit_prepare(model, chunk_len, &vc, &vt))) return rc;
+    const VitTables* d_vt;
+    if ((rc = vit_tables(ctx, model, vt, &d_vt))) return rc;
+    void* ws;
+    const size_t need = viterbi_ws_bytes(nch, chunk_len);
+    if ((rc = ws_get(ctx, WS_VIT, need, &ws))) return rc;
+    CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
+                           d_sign_out, d_score, nullptr, ctx->d_status, s));
+    return CPG_OK;
+}
+
+int cpg_islands_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
+                  int64_t nbases, int64_t chunk_len, cpg_island* d_out, int64_t cap,
+                  int64_t* d_count, void* stream) {
+    if (!ctx || !d_count || (cap > 0 && !d_out)) return set_error(CPG_E_INVALID, "null argument");
+    int rc = check_layout(d_packed, nbases, chunk_len);
+    if (rc) return rc;
+    if (chunk_len % 32) return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 32");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    const int64_t nch = nbases / chunk_len;
+    void* ws;
+    if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &ws))) return rc;
+    CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, 0, ws, ctx->ws[WS_ISL].bytes, d_out,
+                           cap, d_count, pick(ctx, stream)));
+    return CPG_OK;
+}
+
+int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
+                     int64_t nbases, int64_t chunk_len, int64_t first_chunk, cpg_island* d_out,
+                     int64_t cap, int64_t* d_count, void* stream) {
+    if (!ctx || !d_count || (cap > 0 && !d_out)) return set_error(CPG_E_INVALID, "null argument");
+    int rc = check_layout(d_packed, nbases, chunk_len);
+    if (rc) return rc;
+    if (chunk_len % 32) return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 32");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    const int64_t nch = nbases / chunk_len;
+    void* ws;
+    if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &ws))) return rc;
+    CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, first_chunk, ws,
+                           ctx->ws[WS_ISL].bytes, d_out, cap, d_count, pick(ctx, stream)));
+    return CPG_OK;
+}
+
+int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                   int64_t nbases, int64_t chunk_len, double* d_counts, void* stream) {
+    if (!ctx || !model || !d_counts) return set_error(CPG_E_INVALID, "null argument");
+    int rc = check_layout(d_packed, nbases, chunk_len);
+    if (rc) return rc;
+    if (chunk_len % 256) return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 256");
+    if ((rc = model_check_deterministic(model))) return rc;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    const int64_t nch = nbases / chunk_len;
+    void* ws;
+    if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nch, chunk_len), &ws))) return rc;
+    CPG_HIP(launch_estep(*model, d_packed, nch, chunk_len, ws, ctx->ws[WS_EST].bytes,
+                         d_counts, pick(ctx, stream)));
+    return CPG_OK;
+}
+
+// ---- host-buffer entry points -------------------------------------------------------
+#define CPG_TRY(x)              \
+    do {                        \
+        int rc_ = (x);          \
+        if (rc_) return rc_;    \
+    } while (0)
+
+static int stage_in(cpg_ctx* ctx, int slot, const void* src, size_t bytes, void** dev) {
+    CPG_TRY(ws_get(ctx, slot, bytes ? bytes : 16, dev));
+    if (bytes) CPG_HIP(hipMemcpyAsync(*dev, src, bytes, hipMemcpyHostToDevice, ctx->stream));
+    return CPG_OK;
+}
+
+int cpg_count_labelled(cpg_ctx* ctx, const uint32_t* packed, const uint32_t* sign,
+                       int64_t nbases, int64_t chunk_len, cpg_counts_i64* out) {
+    if (!ctx || !packed || !sign || !out) return set_error(CPG_E_INVALID, "null argument");
+    void *dp, *ds, *dc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        CPG_HIP(hipSetDevice(ctx->device));
+        CPG_TRY(stage_in(ctx, WS_IN0, packed, (size_t)((nbases + 15) / 16) * 4, &dp));
+        CPG_TRY(stage_in(ctx, WS_IN1, sign, (size_t)((nbases + 31) / 32) * 4, &ds));
+        CPG_TRY(ws_get(ctx, WS_OUT0, sizeof(cpg_counts_i64), &dc));
+    }
+    CPG_TRY(cpg_count_labelled_d(ctx, (const uint32_t*)dp, (const uint32_t*)ds, nbases, chunk_len,
+                                 (int64_t*)dc, ctx->stream));
+    CPG_HIP(hipMemcpyAsync(out, dc, sizeof *out, hipMemcpyDeviceToHost, ctx->stream));
+    return cpg_sync(ctx, ctx->stream);
+}
+
+int cpg_bw_estep(cpg_ctx* ctx, const cpg_model* model, const uint32_t* packed, int64_t nbases,
+                 int64_t chunk_len, cpg_counts_f64* out) {
+    if (!ctx || !packed || !out || !model) return set_error(CPG_E_INVALID, "null argument");
+    void *dp, *dc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        CPG_HIP(hipSetDevice(ctx->device));
+        CPG_TRY(stage_in(ctx, WS_IN0, packed, (size_t)((nbases + 15) / 16) * 4, &dp));
+        CPG_TRY(ws_get(ctx, WS_OUT0, sizeof(cpg_counts_f64), &dc));
+    }
+    CPG_TRY(cpg_bw_estep_d(ctx, model, (const uint32_t*)dp, nbases, chunk_len, (double*)dc,
+                           ctx->stream));
+    CPG_HIP(hipMemcpyAsync(out, dc, sizeof *out, hipMemcpyDeviceToHost, ctx->stream));
+    return cpg_sync(ctx, ctx->stream);
+}
+
+int cpg_viterbi(cpg_ctx* ctx, const cpg_model* model, const uint32_t* packed, int64_t nbases,
+                int64_t chunk_len, uint32_t* sign_out, double* score) {
+    if (!ctx || !packed || !sign_out || !model) return set_error(CPG_E_INVALID, "null argument");
+    const int64_t nch = chunk_len > 0 ? nbases / chunk_len : 0;
+    void *dp, *dsg, *dsc;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        CPG_HIP(hipSetDevice(ctx->device));
+        CPG_TRY(stage_in(ctx, WS_IN0, packed, (size_t)((nbases + 15) / 16) * 4, &dp));
+        CPG_TRY(ws_get(ctx, WS_OUT0, (size_t)((nbases + 31) / 32) * 4 + 16, &dsg));
+        CPG_TRY(ws_get(ctx, WS_OUT1, (size_t)(nch + 1) * 8, &dsc));
+    }
+    CPG_TRY(cpg_viterbi_d(ctx, model, (const uint32_t*)dp, nbases, chunk_len, (uint32_t*)dsg,
+                          (double*)dsc, ctx->stream));
+    CPG_HIP(hipMemcpyAsync(sign_out, dsg, (size_t)((nbases + 31) / 32) * 4, hipMemcpyDeviceToHost,
+                           ctx->stream));
+    if (score && nch > 0)
+        CPG_HIP(hipMemcpyAsync(score, dsc, (size_t)nch * 8, hipMemcpyDeviceToHost, ctx->stream));
+    return cpg_sync(ctx, ctx->stream);
+}
+
+// HmmEvaluator.decode(model, observations, true) (:260) for one array: obs in 0..3, n >= 1.
+int cpg_decode_states(cpg_ctx* ctx, const cpg_model* model, const int32_t* obs, int64_t n,
+                      int32_t* states_out) {
+    if (!ctx || !model || !obs || !states_out) return set_error(CPG_E_INVALID, "null argument");
+    if (n < 1)
+        return set_error(CPG_E_INVALID,
+                         "empty observation array (reference: NegativeArraySizeException)");
+    std::vector<uint32_t> packed((size_t)(n + 15) / 16 + 4, 0u);
+    for (int64_t i = 0; i < n; ++i) {
+        if (obs[i] < 0 || obs[i] > 3)
+            return set_error(CPG_E_INVALID,
+                             "observation %lld = %d not in 0..3 (reference: "
+                             "ArrayIndexOutOfBoundsException)", (long long)i, obs[i]);
+        packed[i >> 4] |= (uint32_t)obs[i] << ((i & 15) * 2);
+    }
+    std::vector<uint32_t> sign((size_t)(n + 31) / 32 + 4, 0u);
+    double score = 0.0;
+    CPG_TRY(cpg_viterbi(ctx, model, packed.data(), n, n, sign.data(), &score));
+    // pi = 0 for both live states at t=0: Mahout's maxState stays 0 (state A+) at every
+    // step (all candidates are -Double.MAX_VALUE); the '+' sign path is right, the indices
+    // are not the base's: patch them (the final argmax still picks o_{T-1}+ when T > 1).
+    const bool degen = model->pi[obs[0]] == 0.0 && model->pi[obs[0] + 4] == 0.0;
+    for (int64_t i = 0; i < n; ++i) {
+        const bool plus = (sign[i >> 5] >> (i & 31)) & 1u;
+        states_out[i] = obs[i] + (plus ? 0 : 4);
+        if (degen && (i < n - 1 || n == 1)) states_out[i] = 0;
+    }
+    return CPG_OK;
+}
+
+int cpg_islands(cpg_ctx* ctx, const uint32_t* packed, const uint32_t* sign, int64_t nbases,
+                int64_t chunk_len, cpg_island* out, int64_t cap, int64_t* count) {
+    if (!ctx || !packed || !sign || !count || (cap > 0 && !out))
+        return set_error(CPG_E_INVALID, "null argument");
+    void *dp, *ds, *dout, *dcnt;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        CPG_HIP(hipSetDevice(ctx->device));
+        CPG_TRY(stage_in(ctx, WS_IN0, packed, (size_t)((nbases + 15) / 16) * 4, &dp));
+        CPG_TRY(stage_in(ctx, WS_IN1, sign, (size_t)((nbases + 31) / 32) * 4, &ds));
+        CPG_TRY(ws_get(ctx, WS_OUT0, (size_t)(cap > 0 ? cap : 1) * sizeof(cpg_island), &dout));
+        CPG_TRY(ws_get(ctx, WS_OUT1, 16, &dcnt));
+    }
+    CPG_TRY(cpg_islands_d(ctx, (const uint32_t*)dp, (const uint32_t*)ds, nbases, chunk_len,
+                          (cpg_island*)dout, cap, (int64_t*)dcnt, ctx->stream));
+    CPG_HIP(hipMemcpyAsync(count, dcnt, 8, hipMemcpyDeviceToHost, ctx->stream));
+    CPG_TRY(cpg_sync(ctx, ctx->stream));
+    const int64_t n = *count < cap ? *count : cap;
+    if (n > 0)
+        CPG_HIP(hipMemcpy(out, dout, (size_t)n * sizeof(cpg_island), hipMemcpyDeviceToHost));
+    if (*count > cap) return set_error(CPG_E_CAPACITY, "need %lld island records", (long long)*count);
+    return CPG_OK;
+}
+
+}  // extern "C"

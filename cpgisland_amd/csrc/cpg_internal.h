@@ -1,0 +1,114 @@
+// cpg_internal.h — shared declarations of libcpg.so (host side + kernel launchers).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+#include <mutex>
+#include <string>
+
+#include "../../include/cpg.h"
+
+namespace cpg {
+
+// ---- error state (thread-local message behind cpg_last_error) ---------------------
+int set_error(int code, const char* fmt, ...);
+#define CPG_HIP(expr)                                                                  \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            return ::cpg::set_error(CPG_E_DEVICE, "%s failed: %s (%s:%d)", #expr,      \
+                                    hipGetErrorString(e_), __FILE__, __LINE__);        \
+    } while (0)
+
+// ---- geometry ----------------------------------------------------------------------
+constexpr int kSB = 256;            // Viterbi sub-block: positions per lane
+constexpr int kSBWords = kSB / 16;  // packed words per sub-block
+
+// Device status word bits (ctx->d_status), collected by cpg_sync.
+enum : uint32_t {
+    ST_VERIFY_ENTRY = 1u << 0,   // K5 exit value != K4 entry of the next block
+    ST_VERIFY_MAG = 1u << 1,     // K3 composite outside the exact range
+    ST_VERIFY_CHAIN = 1u << 2,   // K7 traceback start state mismatch
+};
+
+// ---- Viterbi constants (host-computed, shared by every kernel) ---------------------
+constexpr int kMaxBinade = 64;
+struct VitConsts {
+    double L[16][4];        // per dinucleotide d = p | b<<2: log a for +->+, -->+, +->-, -->-
+    double logpi[8];
+    int32_t Q[16][4];       // fixed-point L * 2^qshift (rounded)
+    int qshift;
+    double eps;             // bound |approx - exact| on every value of a chunk
+    double spread;          // 2*|min L|: lower slack inside a block
+    int emin, emax;         // binades with exact tables
+    uint64_t tie_mask;      // binade e has a rounding tie -> never regular
+};
+// per-binade rounded constants Le[e][16][4], e in [0, kMaxBinade)
+struct VitTables {
+    double Le[kMaxBinade][16][4];
+};
+
+// Block plan (K2 -> K3/K4)
+enum : int8_t { PLAN_REGULAR = 0, PLAN_SPLIT = 1, PLAN_SEQ = 2, PLAN_DEGEN = 3 };
+struct __attribute__((aligned(8))) VitPlan {
+    int8_t type;
+    int8_t e_pre;
+    int8_t e_post;
+    int8_t pad;
+    uint16_t t1;     // offset (in steps from block's first step) where the window starts
+    uint16_t t2;     // offset where the post composite starts
+};
+
+// ---- context -----------------------------------------------------------------------
+struct Buf {
+    void* p = nullptr;
+    size_t bytes = 0;
+};
+
+}  // namespace cpg
+
+struct cpg_ctx {
+    int device = 0;
+    hipStream_t stream = nullptr;
+    std::mutex mu;
+    uint32_t* d_status = nullptr;     // device status word
+    // workspace (grown on demand; cpg_reserve pre-sizes)
+    cpg::Buf ws[16];
+    // host staging (pinned)
+    cpg::Buf pin[4];
+    // device copies of per-model Viterbi tables
+    static constexpr int kVtSlots = 4;
+    struct VtSlot {
+        cpg_model model;
+        cpg::VitTables* d;
+    } vtc[kVtSlots];
+    int vtn = 0, vtnext = 0;
+};
+
+namespace cpg {
+int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out);
+int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out);
+int model_check_deterministic(const cpg_model* m);
+int vit_prepare(const cpg_model* m, int64_t chunk_len, VitConsts* vc, VitTables* vt);
+
+// kernel launchers (defined in the .hip files); all asynchronous on `s`
+hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
+                        int64_t chunk_len, uint64_t* ws, int64_t* out /*124*/, hipStream_t s);
+size_t count_ws_bytes(int64_t nchunks);
+hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint32_t* packed,
+                          int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
+                          uint32_t* sign_out, double* score, uint8_t* degen,
+                          uint32_t* status, hipStream_t s);
+size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len);
+int64_t vit_nsb(int64_t chunk_len);
+hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
+                          int64_t chunk_len, int64_t first_chunk, void* ws, size_t ws_bytes,
+                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s);
+size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
+hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
+                        int64_t chunk_len, void* ws, size_t ws_bytes, double* out,
+                        hipStream_t s);
+size_t estep_ws_bytes(int64_t nchunks, int64_t chunk_len);
+
+}  // namespace cpg

@@ -1,0 +1,248 @@
+// k_count.hip — labelled int64 counts on gfx950.
+//
+// Training-side counterpart of the BW mapper stripes (init / transition / emission rows,
+// CpGIslandFinder.java:200) computed from hard labels: state s_t = base_t + (sign_t?0:4).
+// Streams 2-bit packed bases (16 B per lane = 64 bases) and sign bits (8 B per lane),
+// builds per-lane dinucleotide bitmasks and counts them with v_bcnt (popcount+add), so a
+// base costs a few VALU ops and no LDS traffic.  Sign classes ride a uniform fast path:
+// inside an island or background run every transition is ++ or --, and only lane-blocks
+// that straddle an island boundary take the general four-class path.
+//
+// Per-workgroup partial counts go to a slab (no global atomics) and a one-workgroup
+// finalize sums the slab in a fixed order and derives emission/dinucleotide/mono counts
+// from the transition + init counts (exact integer identities).
+
+#include "cpg_internal.h"
+
+namespace cpg {
+namespace {
+
+constexpr int kCountThreads = 256;
+constexpr int kRaw = 72;        // tot[16] pp[16] pm[16] mp[16] init[8]
+constexpr uint32_t M55 = 0x55555555u;
+
+struct Masks {
+    uint32_t e[4];   // bit 2k set iff base k == b
+};
+
+__device__ __forceinline__ Masks base_masks(uint32_t w) {
+    uint32_t h = w >> 1;
+    Masks m;
+    m.e[0] = ~(w | h) & M55;
+    m.e[1] = w & ~h & M55;
+    m.e[2] = h & ~w & M55;
+    m.e[3] = w & h & M55;
+    return m;
+}
+
+// spread 16 bits (bit k) to even bit positions (bit 2k)
+__device__ __forceinline__ uint32_t spread16(uint32_t x) {
+    x &= 0xFFFFu;
+    x = (x | (x << 8)) & 0x00FF00FFu;
+    x = (x | (x << 4)) & 0x0F0F0F0Fu;
+    x = (x | (x << 2)) & 0x33333333u;
+    x = (x | (x << 1)) & 0x55555555u;
+    return x;
+}
+
+__global__ __launch_bounds__(kCountThreads) void k_count_main(
+    const uint4* __restrict__ packed4, const uint2* __restrict__ sign2,
+    const uint32_t* __restrict__ packed, const uint32_t* __restrict__ sign, int64_t nblk,
+    int64_t blk_per_chunk, uint64_t* __restrict__ slab) {
+    uint32_t tot[16], pp[16], pm[16], mp[16];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) tot[d] = pp[d] = pm[d] = mp[d] = 0u;
+
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nblk; i += stride) {
+        const uint4 w = packed4[i];
+        const uint2 s = sign2[i];
+        const bool cstart = (i % blk_per_chunk) == 0;
+        uint32_t wprev = 0, sprev = 0;
+        if (!cstart) {
+            wprev = packed[4 * i - 1];
+            sprev = sign[2 * i - 1] >> 31;
+        }
+        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+        Masks cur[4], prv[4];
+#pragma unroll
+        for (int k = 0; k < 4; ++k) cur[k] = base_masks(ww[k]);
+        {
+            uint32_t wp = __builtin_amdgcn_alignbit(ww[0], wprev, 30);
+            prv[0] = base_masks(wp);
+        }
+#pragma unroll
+        for (int k = 1; k < 4; ++k)
+#pragma unroll
+            for (int b = 0; b < 4; ++b)
+                prv[k].e[b] = __builtin_amdgcn_alignbit(cur[k].e[b], cur[k - 1].e[b], 30);
+        if (cstart) {
+#pragma unroll
+            for (int b = 0; b < 4; ++b) prv[0].e[b] &= ~1u;   // no transition into pos 0
+        }
+        const bool all_minus = (s.x == 0u) && (s.y == 0u) && (cstart || sprev == 0u);
+        const bool all_plus = (s.x == ~0u) && (s.y == ~0u) && (cstart || sprev == 1u);
+#pragma unroll
+        for (int k = 0; k < 4; ++k)
+#pragma unroll
+            for (int p = 0; p < 4; ++p)
+#pragma unroll
+                for (int b = 0; b < 4; ++b)
+                    tot[p * 4 + b] += __popc(prv[k].e[p] & cur[k].e[b]);
+        if (!all_minus) {
+            if (all_plus) {
+#pragma unroll
+                for (int k = 0; k < 4; ++k)
+#pragma unroll
+                    for (int p = 0; p < 4; ++p)
+#pragma unroll
+                        for (int b = 0; b < 4; ++b)
+                            pp[p * 4 + b] += __popc(prv[k].e[p] & cur[k].e[b]);
+            } else {
+                // general path: per word spread sign masks
+                const uint32_t sw[4] = {s.x & 0xFFFFu, s.x >> 16, s.y & 0xFFFFu, s.y >> 16};
+                uint32_t sprv = sprev;
+#pragma unroll
+                for (int k = 0; k < 4; ++k) {
+                    uint32_t S = spread16(sw[k]);
+                    uint32_t Sp = (S << 2) | (sprv & 1u);
+                    sprv = sw[k] >> 15;
+                    uint32_t SS = Sp & S, SN = Sp & ~S, NS = ~Sp & S;
+#pragma unroll
+                    for (int p = 0; p < 4; ++p)
+#pragma unroll
+                        for (int b = 0; b < 4; ++b) {
+                            uint32_t D = prv[k].e[p] & cur[k].e[b];
+                            pp[p * 4 + b] += __popc(D & SS);
+                            pm[p * 4 + b] += __popc(D & SN);
+                            mp[p * 4 + b] += __popc(D & NS);
+                        }
+                }
+            }
+        }
+    }
+
+    // wave reduction by recursive halving: after 6 levels lane L holds the wave sum of
+    // counter L (63 shuffles instead of 64 x 6)
+    uint32_t v[64];
+#pragma unroll
+    for (int d = 0; d < 16; ++d) {
+        v[d] = tot[d];
+        v[16 + d] = pp[d];
+        v[32 + d] = pm[d];
+        v[48 + d] = mp[d];
+    }
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int lvl = 0; lvl < 6; ++lvl) {
+        const int o = 32 >> lvl;
+        const bool up = (lane & o) != 0;
+#pragma unroll
+        for (int i = 0; i < o; ++i) {
+            uint32_t send = up ? v[i] : v[i + o];
+            uint32_t keep = up ? v[i + o] : v[i];
+            v[i] = keep + (uint32_t)__shfl_xor((int)send, o);
+        }
+    }
+    __shared__ uint32_t wsum[kCountThreads / 64][64];
+    wsum[threadIdx.x >> 6][lane] = v[0];
+    __syncthreads();
+    if (threadIdx.x < 64) {
+        uint64_t acc = 0;
+#pragma unroll
+        for (int w = 0; w < kCountThreads / 64; ++w) acc += wsum[w][threadIdx.x];
+        slab[(int64_t)blockIdx.x * kRaw + threadIdx.x] = acc;
+    }
+}
+
+// init counts: one thread per chunk, deterministic (no atomics): states of first bases
+__global__ void k_count_init(const uint32_t* __restrict__ packed,
+                             const uint32_t* __restrict__ sign, int64_t nchunks,
+                             int64_t chunk_len, uint32_t* __restrict__ first_state) {
+    int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (c >= nchunks) return;
+    int64_t pos = c * chunk_len;
+    int b = (int)((packed[pos >> 4] >> ((pos & 15) * 2)) & 3u);
+    int s = (int)((sign[pos >> 5] >> (pos & 31)) & 1u);
+    first_state[c] = (uint32_t)(b + (s ? 0 : 4));
+}
+
+__global__ __launch_bounds__(256) void k_count_final(const uint64_t* __restrict__ slab,
+                                                     int nrows,
+                                                     const uint32_t* __restrict__ first_state,
+                                                     int64_t nchunks,
+                                                     int64_t* __restrict__ out) {
+    __shared__ uint64_t raw[kRaw];
+    __shared__ uint64_t initc[8][256];
+    const int t = threadIdx.x;
+    if (t < 64) {
+        uint64_t acc = 0;
+        for (int r = 0; r < nrows; ++r) acc += slab[(int64_t)r * kRaw + t];
+        raw[t] = acc;
+    }
+    uint64_t ic[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t c = t; c < nchunks; c += 256) ic[first_state[c] & 7u]++;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) initc[k][t] = ic[k];
+    __syncthreads();
+    if (t < 8) {
+        uint64_t acc = 0;
+        for (int j = 0; j < 256; ++j) acc += initc[t][j];
+        raw[64 + t] = acc;
+    }
+    __syncthreads();
+    if (t != 0) return;
+    // cpg_counts_i64 layout: init[8] trans[8][8] emit[8][4] dinuc[4][4] mono[4]
+    int64_t* init = out;
+    int64_t* trans = out + 8;
+    int64_t* emit = out + 72;
+    int64_t* dinuc = out + 104;
+    int64_t* mono = out + 120;
+    for (int i = 0; i < 124; ++i) out[i] = 0;
+    for (int s = 0; s < 8; ++s) init[s] = (int64_t)raw[64 + s];
+    for (int p = 0; p < 4; ++p)
+        for (int b = 0; b < 4; ++b) {
+            int d = p * 4 + b;
+            int64_t tt = (int64_t)raw[d], ppv = (int64_t)raw[16 + d],
+                    pmv = (int64_t)raw[32 + d], mpv = (int64_t)raw[48 + d];
+            trans[p * 8 + b] = ppv;
+            trans[p * 8 + b + 4] = pmv;
+            trans[(p + 4) * 8 + b] = mpv;
+            trans[(p + 4) * 8 + b + 4] = tt - ppv - pmv - mpv;
+            dinuc[d] = tt;
+        }
+    for (int s = 0; s < 8; ++s) {
+        int64_t col = init[s];
+        for (int r = 0; r < 8; ++r) col += trans[r * 8 + s];
+        emit[s * 4 + (s & 3)] = col;
+        mono[s & 3] += col;
+    }
+}
+
+}  // namespace
+
+hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
+                        int64_t chunk_len, uint64_t* ws, int64_t* out, hipStream_t s) {
+    const int64_t nblk = nchunks * chunk_len / 64;
+    int grid = 1024;
+    if ((int64_t)grid * kCountThreads > nblk) grid = (int)((nblk + kCountThreads - 1) / kCountThreads);
+    if (grid < 1) grid = 1;
+    uint64_t* slab = ws;
+    uint32_t* first_state = (uint32_t*)(ws + (size_t)1024 * kRaw);
+    if (nblk > 0)
+        hipLaunchKernelGGL(k_count_main, dim3(grid), dim3(kCountThreads), 0, s,
+                           (const uint4*)packed, (const uint2*)sign, packed, sign, nblk,
+                           chunk_len / 64, slab);
+    if (nchunks > 0)
+        hipLaunchKernelGGL(k_count_init, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0,
+                           s, packed, sign, nchunks, chunk_len, first_state);
+    hipLaunchKernelGGL(k_count_final, dim3(1), dim3(256), 0, s, slab, nblk > 0 ? grid : 0,
+                       first_state, nchunks, out);
+    return hipGetLastError();
+}
+
+size_t count_ws_bytes(int64_t nchunks) {
+    return (size_t)1024 * kRaw * 8 + (size_t)(nchunks + 1) * 4;
+}
+
+}  // namespace cpg

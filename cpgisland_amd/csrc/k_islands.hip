@@ -1,0 +1,360 @@
+// k_islands.hip — island scan + filter (CpGIslandFinder.java:262-339) on gfx950.
+//
+// The reference walks each decoded 1 Mi chunk sequentially.  Its state is re-expressed as
+// bit-parallel masks over 32-position words (sign bits + 2-bit packed bases):
+//   start  = S & ~S_prev          (:319-337, inIsland false -> true)
+//   close  = ~S & S_prev          (:273-289, the '-' that ends the island; end = i-1)
+//   C, G   = base masks, CGm = G & C_prev (a G whose predecessor is a C)
+// Island counts are differences of per-word prefix sums; CpG inside (beg, end] is exact
+// from CGm.  The one serial quirk — `atC` is never cleared when an island closes (:325-331),
+// so the first pair of an island can count a CpG against the previous island's last C — is
+// a function stale_in -> stale_out per island (const 0 / const 1 / identity), resolved by a
+// scan over the chunk's islands.  Islands still open at the chunk end are dropped (:269-339
+// never closes them).  Coordinates and (cgCount*islandLen) use Java int arithmetic.
+//
+// Kernels: IA (per chunk) run boundaries + word prefixes; IB (per chunk) per-run stats,
+// stale scan, filter, kept rank; IC (one workgroup) chunk offsets; ID (per chunk) records.
+
+#include "cpg_internal.h"
+
+namespace cpg {
+namespace {
+
+constexpr int kIT = 1024;
+
+__device__ __forceinline__ uint32_t compact16(uint32_t x) {   // even bits -> low 16 bits
+    x &= 0x55555555u;
+    x = (x | (x >> 1)) & 0x33333333u;
+    x = (x | (x >> 2)) & 0x0F0F0F0Fu;
+    x = (x | (x >> 4)) & 0x00FF00FFu;
+    x = (x | (x >> 8)) & 0x0000FFFFu;
+    return x;
+}
+
+struct WordMasks {
+    uint32_t S, start, close, C, G, CG;
+};
+
+// masks of sign word w (positions 32w..32w+31) of a chunk; nw = words in the chunk
+__device__ __forceinline__ WordMasks word_masks(const uint32_t* __restrict__ pk,
+                                                const uint32_t* __restrict__ sg, int64_t w) {
+    WordMasks m;
+    const uint32_t S = sg[w];
+    const uint32_t sprev = w > 0 ? (sg[w - 1] >> 31) : 0u;
+    const uint32_t Sp = (S << 1) | sprev;
+    m.S = S;
+    m.start = S & ~Sp;
+    m.close = ~S & Sp;
+    const uint32_t w0 = pk[2 * w], w1 = pk[2 * w + 1];
+    const uint32_t h0 = w0 >> 1, h1 = w1 >> 1;
+    const uint32_t c = compact16(w0 & ~h0) | (compact16(w1 & ~h1) << 16);   // base == 1
+    const uint32_t g = compact16(h0 & ~w0) | (compact16(h1 & ~w1) << 16);   // base == 2
+    const uint32_t cprev = w > 0 ? ((pk[2 * w - 1] >> 30) == 1u) : 0u;
+    m.C = c;
+    m.G = g;
+    m.CG = g & ((c << 1) | cprev);
+    return m;
+}
+
+struct IslWs {
+    int32_t* Cp;        // per word exclusive prefix (chunk-local)
+    int32_t* Gp;
+    int32_t* CGp;
+    uint32_t* starts;   // per run
+    uint32_t* closes;
+    int32_t* kept;      // per run: rank*2 | stale_in, or -1
+    int32_t* nruns;     // per chunk
+    int32_t* ncloses;
+    int64_t* nkept;
+    int64_t* off;
+    size_t bytes;
+};
+
+IslWs carve_isl(void* base, int64_t nchunks, int64_t C) {
+    const int64_t nw = (C + 31) / 32, maxr = C / 2 + 1;
+    char* p = static_cast<char*>(base);
+    size_t o = 0;
+    auto take = [&](size_t b) {
+        o = (o + 255) & ~size_t(255);
+        char* r = p ? p + o : nullptr;
+        o += b;
+        return r;
+    };
+    IslWs w;
+    w.Cp = (int32_t*)take(nchunks * nw * 4);
+    w.Gp = (int32_t*)take(nchunks * nw * 4);
+    w.CGp = (int32_t*)take(nchunks * nw * 4);
+    w.starts = (uint32_t*)take(nchunks * maxr * 4);
+    w.closes = (uint32_t*)take(nchunks * maxr * 4);
+    w.kept = (int32_t*)take(nchunks * maxr * 4);
+    w.nruns = (int32_t*)take(nchunks * 4);
+    w.ncloses = (int32_t*)take(nchunks * 4);
+    w.nkept = (int64_t*)take(nchunks * 8);
+    w.off = (int64_t*)take((nchunks + 1) * 8);
+    w.bytes = o + 256;
+    return w;
+}
+
+// block-wide exclusive scan of 5 int32 counters (kIT threads)
+struct Cnt5 {
+    int32_t c, g, cg, st, cl;
+};
+
+__global__ __launch_bounds__(kIT) void k_isl_a(const uint32_t* packed, const uint32_t* sign,
+                                               int64_t C, IslWs ws) {
+    const int64_t c = blockIdx.x;
+    const int t = threadIdx.x;
+    const int64_t nw = C / 32;   // C % 32 == 0 (checked on host)
+    const uint32_t* pk = packed + c * (C / 16);
+    const uint32_t* sg = sign + c * nw;
+    const int64_t per = (nw + kIT - 1) / kIT;
+    const int64_t w0 = min((int64_t)t * per, nw), w1 = min(w0 + per, nw);
+    Cnt5 s{0, 0, 0, 0, 0};
+    for (int64_t w = w0; w < w1; ++w) {
+        const WordMasks m = word_masks(pk, sg, w);
+        s.c += __popc(m.C);
+        s.g += __popc(m.G);
+        s.cg += __popc(m.CG);
+        s.st += __popc(m.start);
+        s.cl += __popc(m.close);
+    }
+    __shared__ Cnt5 sb[kIT];
+    sb[t] = s;
+    __syncthreads();
+    for (int off = 1; off < kIT; off <<= 1) {
+        Cnt5 v = sb[t];
+        if (t >= off) {
+            const Cnt5 u = sb[t - off];
+            v.c += u.c; v.g += u.g; v.cg += u.cg; v.st += u.st; v.cl += u.cl;
+        }
+        __syncthreads();
+        sb[t] = v;
+        __syncthreads();
+    }
+    Cnt5 e = t > 0 ? sb[t - 1] : Cnt5{0, 0, 0, 0, 0};
+    const int64_t maxr = C / 2 + 1;
+    int32_t* Cp = ws.Cp + c * nw;
+    int32_t* Gp = ws.Gp + c * nw;
+    int32_t* CGp = ws.CGp + c * nw;
+    uint32_t* st = ws.starts + c * maxr;
+    uint32_t* cl = ws.closes + c * maxr;
+    for (int64_t w = w0; w < w1; ++w) {
+        const WordMasks m = word_masks(pk, sg, w);
+        Cp[w] = e.c;
+        Gp[w] = e.g;
+        CGp[w] = e.cg;
+        e.c += __popc(m.C);
+        e.g += __popc(m.G);
+        e.cg += __popc(m.CG);
+        for (uint32_t x = m.start; x; x &= x - 1) st[e.st++] = (uint32_t)(w * 32 + __ffs(x) - 1);
+        for (uint32_t x = m.close; x; x &= x - 1) cl[e.cl++] = (uint32_t)(w * 32 + __ffs(x) - 1);
+    }
+    if (t == kIT - 1) {
+        ws.nruns[c] = sb[kIT - 1].st;
+        ws.ncloses[c] = sb[kIT - 1].cl;
+#ifdef CPG_DEBUG_ISL
+        printf("isl_a chunk %d: starts %d closes %d C %d G %d CG %d\n", (int)c, sb[kIT - 1].st,
+               sb[kIT - 1].cl, sb[kIT - 1].c, sb[kIT - 1].g, sb[kIT - 1].cg);
+#endif
+    }
+}
+
+__device__ __forceinline__ uint32_t isl_base(const uint32_t* pk, int64_t pos) {
+    return (pk[pos >> 4] >> ((pos & 15) * 2)) & 3u;
+}
+// prefix count of a mask kind (0 C, 1 G, 2 CG) over chunk positions [0, pos)
+__device__ __forceinline__ int32_t pref(const uint32_t* pk, const uint32_t* sg, const int32_t* P,
+                                        int kind, int64_t pos, int64_t nw) {
+    const int64_t w = pos >> 5;
+    if (w >= nw) return P[nw - 1] + __popc(kind == 0 ? word_masks(pk, sg, nw - 1).C
+                                           : kind == 1 ? word_masks(pk, sg, nw - 1).G
+                                                       : word_masks(pk, sg, nw - 1).CG);
+    const WordMasks m = word_masks(pk, sg, w);
+    const uint32_t x = kind == 0 ? m.C : kind == 1 ? m.G : m.CG;
+    const uint32_t lowmask = (pos & 31) ? ((1u << (pos & 31)) - 1u) : 0u;
+    return P[w] + __popc(x & lowmask);
+}
+
+struct RunStat {
+    int32_t beg, end, len, C, G, CGin;
+    uint32_t b0, b1, last;
+};
+__device__ __forceinline__ RunStat run_stat(const uint32_t* pk, const uint32_t* sg, IslWs ws,
+                                            int64_t c, int64_t nw, uint32_t beg, uint32_t close) {
+    RunStat r;
+    r.beg = (int32_t)beg;
+    r.end = (int32_t)close - 1;
+    r.len = (int32_t)(close - beg);
+    const int32_t* Cp = ws.Cp + c * nw;
+    const int32_t* Gp = ws.Gp + c * nw;
+    const int32_t* CGp = ws.CGp + c * nw;
+    r.C = pref(pk, sg, Cp, 0, close, nw) - pref(pk, sg, Cp, 0, beg, nw);
+    r.G = pref(pk, sg, Gp, 1, close, nw) - pref(pk, sg, Gp, 1, beg, nw);
+    r.CGin = r.len >= 2 ? pref(pk, sg, CGp, 2, close, nw) - pref(pk, sg, CGp, 2, beg + 1, nw) : 0;
+    r.b0 = isl_base(pk, beg);
+    r.b1 = r.len >= 2 ? isl_base(pk, beg + 1) : 0u;
+    r.last = isl_base(pk, close - 1);
+    return r;
+}
+// stale atC map (bit x = output for input x): const0 0b00, const1 0b11, id 0b10
+__device__ __forceinline__ uint32_t stale_map(const RunStat& r) {
+    if (r.len >= 2) return r.last == 1u ? 0x3u : 0x0u;
+    return r.b0 == 1u ? 0x3u : 0x2u;
+}
+__device__ __forceinline__ uint32_t mapply(uint32_t m, uint32_t x) { return (m >> x) & 1u; }
+__device__ __forceinline__ uint32_t mcompose(uint32_t f, uint32_t g) {   // f o g
+    return mapply(f, mapply(g, 0)) | (mapply(f, mapply(g, 1)) << 1);
+}
+
+struct Rec {
+    double cg, oe;
+    bool keep;
+    int32_t cpg;
+};
+__device__ __forceinline__ Rec filter(const RunStat& r, uint32_t stale_in) {
+    Rec o;
+    o.cpg = r.CGin + ((r.len >= 2 && r.b1 == 2u && r.b0 != 1u && stale_in) ? 1 : 0);
+    const double ccnt = (double)r.C, gcnt = (double)r.G;
+    o.cg = (ccnt + gcnt) / (double)r.len;                          // :280
+    o.oe = 0.0;
+    if (r.C != 0 && r.G != 0) {                                     // :282-283
+        const int32_t prod = (int32_t)((uint32_t)o.cpg * (uint32_t)r.len);   // int * int wraps
+        o.oe = (double)prod / (ccnt * gcnt);
+    }
+    o.keep = (o.cg > 0.5) && (o.oe > 0.6);                          // :285
+    return o;
+}
+
+__global__ __launch_bounds__(kIT) void k_isl_b(const uint32_t* packed, const uint32_t* sign,
+                                               int64_t C, IslWs ws) {
+    const int64_t c = blockIdx.x;
+    const int t = threadIdx.x;
+    const int64_t nw = C / 32, maxr = C / 2 + 1;
+    const uint32_t* pk = packed + c * (C / 16);
+    const uint32_t* sg = sign + c * nw;
+    const int64_t nr = ws.ncloses[c];   // closed runs only; an open last run is dropped
+    const uint32_t* st = ws.starts + c * maxr;
+    const uint32_t* cl = ws.closes + c * maxr;
+    int32_t* kept = ws.kept + c * maxr;
+    const int64_t per = (nr + kIT - 1) / kIT;
+    const int64_t r0 = min((int64_t)t * per, nr), r1 = min(r0 + per, nr);
+    uint32_t F = 0x2u;
+    for (int64_t r = r0; r < r1; ++r) F = mcompose(stale_map(run_stat(pk, sg, ws, c, nw, st[r], cl[r])), F);
+    __shared__ uint32_t sF[kIT];
+    __shared__ int32_t sK[kIT];
+    sF[t] = F;
+    __syncthreads();
+    for (int off = 1; off < kIT; off <<= 1) {
+        uint32_t x = sF[t];
+        if (t >= off) x = mcompose(x, sF[t - off]);
+        __syncthreads();
+        sF[t] = x;
+        __syncthreads();
+    }
+    uint32_t stale = t > 0 ? mapply(sF[t - 1], 0u) : 0u;   // atC = false at chunk start (:268)
+    int32_t nk = 0;
+    for (int64_t r = r0; r < r1; ++r) {
+        const RunStat rs = run_stat(pk, sg, ws, c, nw, st[r], cl[r]);
+        const Rec o = filter(rs, stale);
+        kept[r] = o.keep ? (int32_t)(stale) : -1;   // rank added below
+#ifdef CPG_DEBUG_ISL
+        if (c == 0 && r < 8)
+            printf("run %d beg %d end %d len %d C %d G %d CGin %d b0 %u b1 %u last %u cg %f oe %f keep %d\n",
+                   (int)r, rs.beg, rs.end, rs.len, rs.C, rs.G, rs.CGin, rs.b0, rs.b1, rs.last, o.cg, o.oe, (int)o.keep);
+#endif
+        nk += o.keep;
+        stale = mapply(stale_map(rs), stale);
+    }
+    sK[t] = nk;
+    __syncthreads();
+    for (int off = 1; off < kIT; off <<= 1) {
+        int32_t x = sK[t];
+        if (t >= off) x += sK[t - off];
+        __syncthreads();
+        sK[t] = x;
+        __syncthreads();
+    }
+    int32_t rank = t > 0 ? sK[t - 1] : 0;
+    for (int64_t r = r0; r < r1; ++r)
+        if (kept[r] >= 0) kept[r] |= (rank++) << 1;
+    if (t == kIT - 1) ws.nkept[c] = sK[kIT - 1];
+}
+
+__global__ __launch_bounds__(kIT) void k_isl_c(int64_t nchunks, IslWs ws, int64_t* count) {
+    const int t = threadIdx.x;
+    const int64_t per = (nchunks + kIT - 1) / kIT;
+    const int64_t c0 = min((int64_t)t * per, nchunks), c1 = min(c0 + per, nchunks);
+    int64_t s = 0;
+    for (int64_t c = c0; c < c1; ++c) s += ws.nkept[c];
+    __shared__ int64_t sb[kIT];
+    sb[t] = s;
+    __syncthreads();
+    for (int off = 1; off < kIT; off <<= 1) {
+        int64_t x = sb[t];
+        if (t >= off) x += sb[t - off];
+        __syncthreads();
+        sb[t] = x;
+        __syncthreads();
+    }
+    int64_t o = t > 0 ? sb[t - 1] : 0;
+    for (int64_t c = c0; c < c1; ++c) {
+        ws.off[c] = o;
+        o += ws.nkept[c];
+    }
+    if (t == kIT - 1) *count = sb[kIT - 1];
+}
+
+__global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, const uint32_t* sign,
+                                               int64_t C, int64_t first_chunk, IslWs ws,
+                                               cpg_island* out, int64_t cap) {
+    const int64_t c = blockIdx.x;
+    const int64_t nw = C / 32, maxr = C / 2 + 1;
+    const uint32_t* pk = packed + c * (C / 16);
+    const uint32_t* sg = sign + c * nw;
+    const int64_t nr = ws.ncloses[c];
+    const uint32_t* st = ws.starts + c * maxr;
+    const uint32_t* cl = ws.closes + c * maxr;
+    const int32_t* kept = ws.kept + c * maxr;
+    const int64_t gchunk = first_chunk + c;
+    const uint32_t cbase = (uint32_t)gchunk * (uint32_t)C;   // chunk*0x100000, Java int
+    for (int64_t r = threadIdx.x; r < nr; r += kIT) {
+        const int32_t k = kept[r];
+        if (k < 0) continue;
+        const int64_t dst = ws.off[c] + (k >> 1);
+        if (dst >= cap) continue;
+        const RunStat rs = run_stat(pk, sg, ws, c, nw, st[r], cl[r]);
+        const Rec o = filter(rs, (uint32_t)(k & 1));
+        cpg_island isl;
+        isl.beg1 = (int32_t)((uint32_t)rs.beg + cbase + 1u);          // :287
+        isl.end1 = (int32_t)((uint32_t)rs.end + cbase + 1u);
+        isl.len = rs.len;
+        isl.chunk = (int32_t)gchunk;
+        isl.cg = o.cg;
+        isl.oe = o.oe;
+        out[dst] = isl;
+    }
+}
+
+}  // namespace
+
+size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len) {
+    return carve_isl(nullptr, nchunks, chunk_len).bytes;
+}
+
+hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
+                          int64_t chunk_len, int64_t first_chunk, void* wsp, size_t ws_bytes,
+                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s) {
+    IslWs ws = carve_isl(wsp, nchunks, chunk_len);
+    if (ws.bytes > ws_bytes) return hipErrorInvalidValue;
+    if (nchunks == 0) return hipMemsetAsync(count, 0, sizeof(int64_t), s);
+    hipLaunchKernelGGL(k_isl_a, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
+                       chunk_len, ws);
+    hipLaunchKernelGGL(k_isl_b, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
+                       chunk_len, ws);
+    hipLaunchKernelGGL(k_isl_c, dim3(1), dim3(kIT), 0, s, nchunks, ws, count);
+    hipLaunchKernelGGL(k_isl_d, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
+                       chunk_len, first_chunk, ws, out, cap);
+    return hipGetLastError();
+}
+
+}  // namespace cpg

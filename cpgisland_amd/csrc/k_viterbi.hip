@@ -1,0 +1,777 @@
+// k_viterbi.hip — exact parallel Viterbi for the CpG-island HMM on gfx950.
+//
+// Replaces HmmEvaluator.decode(trainedModel, testSequence, true)
+// (/root/reference/CpGIslandFinder.java:260; Mahout HmmAlgorithms.viterbiAlgorithm,
+// scaled=true) applied to every whole chunk (:256-260).  Result: the state path, bit-for-bit
+// the one the sequential fp64 recurrence produces (Mahout operation order, '>' tie-break),
+// not an approximation of it.
+//
+// Why a parallel scan can be exact here:
+//   With the deterministic emission matrix only the two states (o_t,+) and (o_t,-) are live,
+//   so the recurrence is a 2x2 max-plus product per step with constants L[dinucleotide].
+//   fp64 addition is not associative in general — but while every value of a stretch of the
+//   recurrence lies in one binade [2^e, 2^(e+1)) (values are negative: in magnitude), every
+//   double there is a multiple of u_e = 2^(e-52), so fl(x + L) = x + RN_e(L) exactly (RN_e
+//   = round to a multiple of u_e; host checks that no constant sits on a rounding tie).
+//   Within a binade the recurrence is therefore EXACT max-plus arithmetic over the rounded
+//   constants, which is associative: sub-block composites can be combined in any order.
+//
+// Pipeline (one lane = one 256-position sub-block "block"):
+//   K1 approx composite   int32 fixed-point 2x2 composite per block
+//   K2 plan               per chunk: scan of K1 composites -> approximate values at every
+//                         block boundary (error <= eps, bounded on the host); classify each
+//                         block: REGULAR (inside one binade), SPLIT (one binade crossing:
+//                         exact prefix composite + short sequential window + exact suffix
+//                         composite), SEQ (sequential), DEGEN (pi = 0 for both live states)
+//   K3/K3b exact composite fp64 composites with the binade-rounded constants (exact)
+//   K4 chain              per chunk: segmented scan of exact composites; ONE lane walks the
+//                         few barriers (windows / SEQ blocks) sequentially with the original
+//                         constants; exact entry value of every block
+//   K5 re-forward         per block from its exact entry with the ORIGINAL constants, the
+//                         reference's own step (same rounding, same '>' tie-break): 2-bit
+//                         backpointers; the exit value must equal the next block's entry
+//                         bit-for-bit (self-check -> status word)
+//   K6 trace scan         per chunk: final argmax + suffix scan of block origin maps
+//   K7 traceback          per block: state path -> sign bits
+//
+// Layout: packed bases (16/uint32, base k at bits 2k), sign bits (32/uint32), all in HBM.
+// Dinucleotide code d = prev | cur << 2 (one bfe of the packed word).
+
+#include <cfloat>
+#include <cmath>
+
+#include "cpg_internal.h"
+
+namespace cpg {
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int32_t kNeg32 = -(1 << 30);
+constexpr int64_t kNeg64 = -(1ll << 60);
+
+// 2x2 max-plus matrices: rows = start state (0 '+', 1 '-'), cols = end state.
+struct C64 {
+    double pp, pm, mp, mm;
+};
+struct CI {
+    int64_t pp, pm, mp, mm;
+};
+
+__device__ __forceinline__ C64 c64_id() { return {0.0, -INFINITY, -INFINITY, 0.0}; }
+__device__ __forceinline__ CI ci_id() { return {0, kNeg64, kNeg64, 0}; }
+
+// one step of the composite with constants l = (+->+, -->+, +->-, -->-)
+__device__ __forceinline__ void c64_step(C64& c, double l0, double l1, double l2, double l3) {
+    double npp = fmax(c.pp + l0, c.pm + l1);
+    double npm = fmax(c.pp + l2, c.pm + l3);
+    double nmp = fmax(c.mp + l0, c.mm + l1);
+    double nmm = fmax(c.mp + l2, c.mm + l3);
+    c = {npp, npm, nmp, nmm};
+}
+__device__ __forceinline__ C64 c64_mul(const C64& a, const C64& b) {
+    return {fmax(a.pp + b.pp, a.pm + b.mp), fmax(a.pp + b.pm, a.pm + b.mm),
+            fmax(a.mp + b.pp, a.mm + b.mp), fmax(a.mp + b.pm, a.mm + b.mm)};
+}
+__device__ __forceinline__ double2 c64_apply(double2 v, const C64& c) {
+    return make_double2(fmax(v.x + c.pp, v.y + c.mp), fmax(v.x + c.pm, v.y + c.mm));
+}
+__device__ __forceinline__ int64_t cl(int64_t x) { return x < kNeg64 ? kNeg64 : x; }
+__device__ __forceinline__ int64_t mx(int64_t a, int64_t b) { return a > b ? a : b; }
+__device__ __forceinline__ CI ci_mul(const CI& a, const CI& b) {
+    return {cl(mx(a.pp + b.pp, a.pm + b.mp)), cl(mx(a.pp + b.pm, a.pm + b.mm)),
+            cl(mx(a.mp + b.pp, a.mm + b.mp)), cl(mx(a.mp + b.pm, a.mm + b.mm))};
+}
+__device__ __forceinline__ void ci_apply(int64_t& P, int64_t& M, const CI& c) {
+    int64_t nP = cl(mx(P + c.pp, M + c.mp)), nM = cl(mx(P + c.pm, M + c.mm));
+    P = nP;
+    M = nM;
+}
+
+// The reference step (Mahout order): target '+' sees predecessor '+' first, so '-' wins
+// only when strictly greater; + log(1.0) = +0.0 is exact and omitted.
+struct Step {
+    double P, M;
+    uint32_t bP, bM;   // 1: predecessor is '-'
+};
+__device__ __forceinline__ Step ref_step(double P, double M, double l0, double l1, double l2,
+                                         double l3) {
+    double cpp = P + l0, cmp = M + l1, cpm = P + l2, cmm = M + l3;
+    Step s;
+    s.bP = cmp > cpp;
+    s.bM = cmm > cpm;
+    s.P = s.bP ? cmp : cpp;
+    s.M = s.bM ? cmm : cpm;
+    return s;
+}
+
+__device__ __forceinline__ uint32_t base_at(const uint32_t* __restrict__ pk, int64_t pos) {
+    return (pk[pos >> 4] >> ((pos & 15) * 2)) & 3u;
+}
+
+// Walk the steps of block k (positions k*256 .. k*256+255 of the chunk, position 0 and
+// positions >= C excluded).  f(d, q, jj): d = dinucleotide code, q = quad (64 positions),
+// jj = position within the quad (compile-time).
+template <bool kFull, class F>
+__device__ __forceinline__ void walk_block(const uint32_t* __restrict__ pk, int64_t k, int64_t C,
+                                           F&& f) {
+    const int64_t wbase = k * kSBWords;
+    const int64_t nwords = (C + 15) >> 4;
+    uint32_t prev = (k > 0) ? pk[wbase - 1] : 0u;
+#pragma unroll 1
+    for (int q = 0; q < 4; ++q) {
+        uint32_t w[4];
+        if (kFull) {
+            const uint4 v = *reinterpret_cast<const uint4*>(pk + wbase + 4 * q);
+            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+        } else {
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t wi = wbase + 4 * q + r;
+                w[r] = wi < nwords ? pk[wi] : 0u;
+            }
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) {
+                const int jj = r * 16 + i;
+                const uint32_t d = (i == 0) ? (__builtin_amdgcn_alignbit(w[r], prev, 30) & 15u)
+                                            : ((w[r] >> (2 * i - 2)) & 15u);
+                if (kFull) {
+                    f(d, q, jj);
+                } else {
+                    const int64_t pos = k * kSB + q * 64 + jj;
+                    if (pos >= 1 && pos < C) f(d, q, jj);
+                }
+            }
+            prev = w[r];
+        }
+    }
+}
+
+struct Geo {
+    int64_t nchunks, C, nsb;
+    __device__ __forceinline__ bool full(int64_t k) const { return k > 0 && (k + 1) * kSB <= C; }
+    __device__ __forceinline__ int jfirst(int64_t k) const { return k == 0 ? 1 : 0; }
+    __device__ __forceinline__ int jend(int64_t k) const {
+        int64_t e = C - k * kSB;
+        return (int)(e < kSB ? (e < 0 ? 0 : e) : kSB);
+    }
+};
+
+__device__ __forceinline__ const uint32_t* chunk_ptr(const uint32_t* packed, const Geo& g,
+                                                     int64_t c) {
+    return packed + c * (g.C >> 4);   // C % 256 == 0 whenever nchunks > 1
+}
+
+// ---------------------------------------------------------------- K1: approx composite
+__global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uint32_t* packed,
+                                                         Geo g, int4* __restrict__ comp) {
+    __shared__ int4 Q[16];
+    if (threadIdx.x < 16)
+        Q[threadIdx.x] = make_int4(vc.Q[threadIdx.x][0], vc.Q[threadIdx.x][1],
+                                   vc.Q[threadIdx.x][2], vc.Q[threadIdx.x][3]);
+    __syncthreads();
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gid >= g.nchunks * g.nsb) return;
+    const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
+    const uint32_t* pk = chunk_ptr(packed, g, c);
+    int32_t a = 0, b = kNeg32, e = kNeg32, f = 0;
+    auto step = [&](uint32_t d, int, int) {
+        const int4 q = Q[d];
+        int32_t na = max(a + q.x, b + q.y), nb = max(a + q.z, b + q.w);
+        int32_t ne = max(e + q.x, f + q.y), nf = max(e + q.z, f + q.w);
+        a = na; b = nb; e = ne; f = nf;
+    };
+    if (g.full(k)) walk_block<true>(pk, k, g.C, step);
+    else walk_block<false>(pk, k, g.C, step);
+    comp[gid] = make_int4(a, b, e, f);
+}
+
+// ---------------------------------------------------------------- K2: plan
+__device__ __forceinline__ int64_t fix_of(double x, int f) {
+    if (!(x > -INFINITY)) return kNeg64;
+    return (int64_t)llrint(ldexp(x, f));
+}
+__device__ __forceinline__ bool binade_ok(const VitConsts& vc, int e) {
+    return e >= vc.emin && e <= vc.emax && !((vc.tie_mask >> e) & 1ull);
+}
+
+__global__ __launch_bounds__(kThreads) void k_vit_plan(VitConsts vc, const uint32_t* packed,
+                                                       Geo g, const int4* __restrict__ comp,
+                                                       VitPlan* __restrict__ plan,
+                                                       uint8_t* __restrict__ degen,
+                                                       int32_t* __restrict__ splitlist,
+                                                       int32_t* __restrict__ splitcount) {
+    const int64_t c = blockIdx.x;
+    const int t = threadIdx.x;
+    const uint32_t* pk = chunk_ptr(packed, g, c);
+    const int4* cc = comp + c * g.nsb;
+    VitPlan* pl = plan + c * g.nsb;
+    __shared__ CI buf[kThreads];
+    __shared__ int4 Q[16];
+    __shared__ int nsplit;
+    if (t < 16) Q[t] = make_int4(vc.Q[t][0], vc.Q[t][1], vc.Q[t][2], vc.Q[t][3]);
+    if (t == 0) nsplit = 0;
+    const int64_t per = (g.nsb + kThreads - 1) / kThreads;
+    const int64_t b0 = t * per, b1 = min(b0 + per, g.nsb);
+
+    const uint32_t o0 = base_at(pk, 0);
+    const double lp = vc.logpi[o0], lm = vc.logpi[o0 + 4];
+    const bool dg = !(lp > -INFINITY) && !(lm > -INFINITY);
+    if (t == 0) degen[c] = dg ? 1 : 0;
+    if (dg) {
+        for (int64_t k = b0; k < b1; ++k) pl[k] = VitPlan{PLAN_DEGEN, 0, 0, 0, 0, 0};
+        if (t == 0) splitcount[c] = 0;
+        return;
+    }
+    CI prod = ci_id();
+    for (int64_t k = b0; k < b1; ++k) {
+        const int4 x = cc[k];
+        prod = ci_mul(prod, CI{x.x, x.y, x.z, x.w});
+    }
+    buf[t] = prod;
+    __syncthreads();
+    for (int off = 1; off < kThreads; off <<= 1) {
+        CI v = buf[t];
+        if (t >= off) v = ci_mul(buf[t - off], v);
+        __syncthreads();
+        buf[t] = v;
+        __syncthreads();
+    }
+    const CI excl = t > 0 ? buf[t - 1] : ci_id();
+    const int f = vc.qshift;
+    const double S = ldexp(1.0, f), invS = 1.0 / S;
+    const double epsc = vc.eps + invS;   // candidates: + constant rounding
+    int64_t P = fix_of(lp, f), M = fix_of(lm, f);
+    ci_apply(P, M, excl);
+    for (int64_t k = b0; k < b1; ++k) {
+        const int64_t eP = P, eM = M;
+        const int4 x = cc[k];
+        ci_apply(P, M, CI{x.x, x.y, x.z, x.w});
+        VitPlan p{PLAN_SEQ, 0, 0, 0, 0, 0};
+        const int j0 = g.jfirst(k), jend = g.jend(k);
+        if (k > 0 && jend > j0) {
+            const double hi = (double)mx(eP, eM) * invS + vc.eps;
+            const double lo = (double)mx(P, M) * invS - vc.eps - vc.spread;
+            if (hi < 0.0) {
+                const int e = ilogb(-hi);
+                if (binade_ok(vc, e) && lo > -ldexp(1.0, e + 1)) {
+                    p = VitPlan{PLAN_REGULAR, (int8_t)e, 0, 0, (uint16_t)jend, (uint16_t)jend};
+                } else {
+                    // locate the crossing with the approximate recurrence
+                    const bool okA = binade_ok(vc, e), okB = binade_ok(vc, e + 1);
+                    const double loA = -ldexp(1.0, e + 1), hiA = -ldexp(1.0, e);
+                    const double loB = -ldexp(1.0, e + 2), hiB = loA;
+                    int t1 = -1, lastbad = j0 - 1;
+                    int64_t aP = eP, aM = eM;
+                    auto scan = [&](uint32_t d, int q, int jj) {
+                        const int j = q * 64 + jj;
+                        const int4 qq = Q[d];
+                        const int64_t c0 = aP + qq.x, c1 = aM + qq.y, c2 = aP + qq.z,
+                                      c3 = aM + qq.w;
+                        const double vmax = (double)mx(aP, aM) * invS + epsc;
+                        const double vmin =
+                            (double)min(min(min(c0, c1), min(c2, c3)), min(aP, aM)) * invS - epsc;
+                        const bool regA = okA && vmax <= hiA && vmin > loA;
+                        const bool regB = okB && vmax <= hiB && vmin > loB;
+                        if (!regA && t1 < 0) t1 = j;
+                        if (!regB) lastbad = j;
+                        aP = mx(c0, c1);
+                        aM = mx(c2, c3);
+                    };
+                    if (g.full(k)) walk_block<true>(pk, k, g.C, scan);
+                    else walk_block<false>(pk, k, g.C, scan);
+                    if (t1 < 0) t1 = jend;
+                    int t2 = lastbad + 1;
+                    if (!okA) t1 = j0;
+                    if (!okB) t2 = jend;
+                    if (t2 < t1) t2 = t1;
+                    if (!(t1 == j0 && t2 == jend))
+                        p = VitPlan{PLAN_SPLIT, (int8_t)e, (int8_t)(e + 1), 0, (uint16_t)t1,
+                                    (uint16_t)t2};
+                }
+            }
+        }
+        pl[k] = p;
+        if (p.type == PLAN_SPLIT) {
+            int slot = atomicAdd(&nsplit, 1);
+            splitlist[c * g.nsb + slot] = (int32_t)k;
+        }
+    }
+    __syncthreads();
+    if (t == 0) splitcount[c] = nsplit;
+}
+
+// ---------------------------------------------------------------- K3: exact composites
+// comp3 per block: pre (4 doubles) | post (4 doubles)
+__device__ __forceinline__ double c64_absmax(const C64& c) {
+    return fmax(fmax(fabs(c.pp), fabs(c.pm)), fmax(fabs(c.mp), fabs(c.mm)));
+}
+__device__ __forceinline__ bool c64_exact(const C64& c, int e, double spread) {
+    return c64_absmax(c) + spread < ldexp(1.0, e + 1);
+}
+
+__global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitTables* vt,
+                                                        const uint32_t* packed, Geo g,
+                                                        VitPlan* __restrict__ plan,
+                                                        double4* __restrict__ comp3,
+                                                        uint32_t* status) {
+    extern __shared__ __attribute__((aligned(16))) double4 sLe[];   // [e - emin][16]
+    const int nb = vc.emax - vc.emin + 1;
+    for (int i = threadIdx.x; i < nb * 16; i += kThreads) {
+        const double* s = vt->Le[vc.emin + i / 16][i % 16];
+        sLe[i] = make_double4(s[0], s[1], s[2], s[3]);
+    }
+    __syncthreads();
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gid >= g.nchunks * g.nsb) return;
+    const VitPlan p = plan[gid];
+    if (p.type != PLAN_REGULAR) return;
+    const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
+    const uint32_t* pk = chunk_ptr(packed, g, c);
+    const double4* tab = sLe + (p.e_pre - vc.emin) * 16;
+    C64 acc = c64_id();
+    auto step = [&](uint32_t d, int, int) {
+        const double4 l = tab[d];
+        c64_step(acc, l.x, l.y, l.z, l.w);
+    };
+    if (g.full(k)) walk_block<true>(pk, k, g.C, step);
+    else walk_block<false>(pk, k, g.C, step);
+    if (!c64_exact(acc, p.e_pre, vc.spread)) {
+        plan[gid].type = PLAN_SEQ;   // exactness not guaranteed: let K4 run it sequentially
+        return;
+    }
+    comp3[gid * 2] = make_double4(acc.pp, acc.pm, acc.mp, acc.mm);
+    comp3[gid * 2 + 1] = make_double4(0.0, -INFINITY, -INFINITY, 0.0);
+}
+
+// split blocks: pre composite on [jfirst, t1) at e_pre, post composite on [t2, jend) at e_post
+__global__ __launch_bounds__(64) void k_vit_exact_split(VitConsts vc, const VitTables* vt,
+                                                        const uint32_t* packed, Geo g,
+                                                        VitPlan* __restrict__ plan,
+                                                        const int32_t* __restrict__ splitlist,
+                                                        const int32_t* __restrict__ splitcount,
+                                                        double4* __restrict__ comp3) {
+    const int64_t c = blockIdx.x;
+    const int n = splitcount[c];
+    const uint32_t* pk = chunk_ptr(packed, g, c);
+    for (int i = threadIdx.x; i < n; i += 64) {
+        const int64_t k = splitlist[c * g.nsb + i];
+        const int64_t gid = c * g.nsb + k;
+        VitPlan p = plan[gid];
+        const double(*ta)[4] = vt->Le[p.e_pre];
+        const double(*tb)[4] = vt->Le[p.e_post];
+        C64 pre = c64_id(), post = c64_id();
+        const int t1 = p.t1, t2 = p.t2;
+        auto step = [&](uint32_t d, int q, int jj) {
+            const int j = q * 64 + jj;
+            if (j < t1) c64_step(pre, ta[d][0], ta[d][1], ta[d][2], ta[d][3]);
+            else if (j >= t2) c64_step(post, tb[d][0], tb[d][1], tb[d][2], tb[d][3]);
+        };
+        if (g.full(k)) walk_block<true>(pk, k, g.C, step);
+        else walk_block<false>(pk, k, g.C, step);
+        if (!c64_exact(pre, p.e_pre, vc.spread) || !c64_exact(post, p.e_post, vc.spread)) {
+            plan[gid].type = PLAN_SEQ;
+            continue;
+        }
+        comp3[gid * 2] = make_double4(pre.pp, pre.pm, pre.mp, pre.mm);
+        comp3[gid * 2 + 1] = make_double4(post.pp, post.pm, post.mp, post.mm);
+    }
+}
+
+// ---------------------------------------------------------------- K4: chain
+__device__ __forceinline__ C64 ld_c64(const double4* p) {
+    const double4 x = *p;
+    return {x.x, x.y, x.z, x.w};
+}
+__device__ __forceinline__ void st_c64(double4* p, const C64& c) {
+    *p = make_double4(c.pp, c.pm, c.mp, c.mm);
+}
+
+// sequential reference steps over positions [k*256 + ja, k*256 + jb) of the chunk
+__device__ double2 seq_steps(const uint32_t* __restrict__ pk, const double4* L, int64_t k,
+                             int ja, int jb, double2 v) {
+    if (jb <= ja) return v;
+    int64_t pos = k * kSB + ja;
+    uint32_t w = pk[pos >> 4];
+    uint32_t prevb = base_at(pk, pos - 1);
+    double P = v.x, M = v.y;
+    for (int j = ja; j < jb; ++j, ++pos) {
+        if ((pos & 15) == 0) w = pk[pos >> 4];
+        const uint32_t b = (w >> ((pos & 15) * 2)) & 3u;
+        const uint32_t d = prevb | (b << 2);
+        const double4 l = L[d];
+        const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
+        P = s.P;
+        M = s.M;
+        prevb = b;
+    }
+    return make_double2(P, M);
+}
+
+__global__ __launch_bounds__(kThreads) void k_vit_chain(
+    VitConsts vc, const uint32_t* packed, Geo g, const VitPlan* __restrict__ plan,
+    const double4* __restrict__ comp3, const uint8_t* __restrict__ degen,
+    double2* __restrict__ entry, double4* __restrict__ gk, double4* __restrict__ gap,
+    int32_t* __restrict__ barlist, double2* __restrict__ vout) {
+    const int64_t c = blockIdx.x;
+    const int t = threadIdx.x;
+    const int64_t per = (g.nsb + kThreads - 1) / kThreads;
+    const int64_t b0 = t * per, b1 = min(b0 + per, g.nsb);
+    double2* ent = entry + c * (g.nsb + 1);
+    __shared__ double4 sL[16];
+    if (t < 16) sL[t] = make_double4(vc.L[t][0], vc.L[t][1], vc.L[t][2], vc.L[t][3]);
+    if (degen[c]) {
+        for (int64_t k = b0; k < b1; ++k) ent[k] = make_double2(-DBL_MAX, -DBL_MAX);
+        if (t == kThreads - 1) ent[g.nsb] = make_double2(-DBL_MAX, -DBL_MAX);
+        return;
+    }
+    const uint32_t* pk = chunk_ptr(packed, g, c);
+    const VitPlan* pl = plan + c * g.nsb;
+    const double4* cp = comp3 + c * g.nsb * 2;
+    double4* gkc = gk + c * g.nsb;
+    double4* gpc = gap + c * g.nsb;
+    int32_t* blc = barlist + c * g.nsb;
+    double2* voc = vout + c * g.nsb;
+
+    // phase 1: thread-local pieces
+    C64 run = c64_id(), lead = c64_id();
+    bool hasb = false;
+    int nb = 0;
+    for (int64_t k = b0; k < b1; ++k) {
+        const VitPlan p = pl[k];
+        if (p.type == PLAN_REGULAR) {
+            run = c64_mul(run, ld_c64(cp + 2 * k));
+        } else {
+            if (p.type == PLAN_SPLIT) run = c64_mul(run, ld_c64(cp + 2 * k));
+            if (!hasb) lead = run;
+            else st_c64(gkc + k, run);
+            hasb = true;
+            ++nb;
+            run = (p.type == PLAN_SPLIT) ? ld_c64(cp + 2 * k + 1) : c64_id();
+        }
+    }
+    if (!hasb) lead = run;
+    // phase 2: segmented scan of (hasb, trail) + barrier count scan
+    __shared__ C64 sM[kThreads];
+    __shared__ int sF[kThreads];
+    __shared__ int sN[kThreads];
+    sM[t] = run;
+    sF[t] = hasb;
+    sN[t] = nb;
+    __syncthreads();
+    for (int off = 1; off < kThreads; off <<= 1) {
+        C64 m = sM[t];
+        int fl = sF[t], n = sN[t];
+        if (t >= off) {
+            if (!fl) m = c64_mul(sM[t - off], m);
+            fl |= sF[t - off];
+            n += sN[t - off];
+        }
+        __syncthreads();
+        sM[t] = m;
+        sF[t] = fl;
+        sN[t] = n;
+        __syncthreads();
+    }
+    const C64 incoming = t > 0 ? sM[t - 1] : c64_id();
+    const int bidx0 = t > 0 ? sN[t - 1] : 0;
+    const int nbar = sN[kThreads - 1];
+    // barrier list in chunk order
+    {
+        int idx = bidx0;
+        bool first = true;
+        for (int64_t k = b0; k < b1; ++k) {
+            const VitPlan p = pl[k];
+            if (p.type == PLAN_SPLIT || p.type == PLAN_SEQ) {
+                blc[idx] = (int32_t)k;
+                if (first) st_c64(gpc + idx, c64_mul(incoming, lead));
+                else st_c64(gpc + idx, ld_c64(gkc + k));
+                first = false;
+                ++idx;
+            }
+        }
+    }
+    __syncthreads();
+    // phase 3: the serial chain over barriers (one lane)
+    const uint32_t o0 = base_at(pk, 0);
+    const double2 init = make_double2(vc.logpi[o0], vc.logpi[o0 + 4]);
+    if (t == 0) {
+        double2 v = init;
+        for (int i = 0; i < nbar; ++i) {
+            const int64_t k = blc[i];
+            const VitPlan p = pl[k];
+            v = c64_apply(v, ld_c64(gpc + i));
+            const int ja = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
+            const int jb = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
+            v = seq_steps(pk, sL, k, ja, jb, v);
+            voc[i] = v;
+        }
+    }
+    __syncthreads();
+    // phase 4: entries
+    double2 v = (bidx0 > 0) ? voc[bidx0 - 1] : init;
+    if (t > 0) v = c64_apply(v, incoming);
+    int idx = bidx0;
+    for (int64_t k = b0; k < b1; ++k) {
+        ent[k] = v;
+        const VitPlan p = pl[k];
+        if (p.type == PLAN_REGULAR) {
+            v = c64_apply(v, ld_c64(cp + 2 * k));
+        } else {
+            v = voc[idx++];
+            if (p.type == PLAN_SPLIT) v = c64_apply(v, ld_c64(cp + 2 * k + 1));
+        }
+    }
+    if (b1 == g.nsb && b0 < b1) ent[g.nsb] = v;
+}
+
+// ---------------------------------------------------------------- K5: re-forward
+__global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const uint32_t* packed,
+                                                          Geo g, const uint8_t* __restrict__ degen,
+                                                          const double2* __restrict__ entry,
+                                                          uint4* __restrict__ bp,
+                                                          uint8_t* __restrict__ origin,
+                                                          uint32_t* status) {
+    __shared__ double4 L[16];
+    if (threadIdx.x < 16)
+        L[threadIdx.x] = make_double4(vc.L[threadIdx.x][0], vc.L[threadIdx.x][1],
+                                      vc.L[threadIdx.x][2], vc.L[threadIdx.x][3]);
+    __syncthreads();
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gid >= g.nchunks * g.nsb) return;
+    const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
+    uint4* bpo = bp + gid * 4;   // words 0..7 bpP, 8..15 bpM
+    if (degen[c]) {
+        for (int i = 0; i < 4; ++i) bpo[i] = make_uint4(0, 0, 0, 0);
+        origin[gid] = 0x2;   // identity
+        return;
+    }
+    const uint32_t* pk = chunk_ptr(packed, g, c);
+    const double2* ent = entry + c * (g.nsb + 1);
+    const double2 v0 = ent[k];
+    double P = v0.x, M = v0.y;
+    uint32_t oP = 1u, oM = 0u;   // origin sign of the current '+' / '-' survivor
+    uint32_t wP0 = 0, wP1 = 0, wM0 = 0, wM1 = 0;
+    auto flush = [&](int q) {
+        uint32_t* o = reinterpret_cast<uint32_t*>(bpo);
+        o[2 * q] = wP0; o[2 * q + 1] = wP1; o[8 + 2 * q] = wM0; o[8 + 2 * q + 1] = wM1;
+        wP0 = wP1 = wM0 = wM1 = 0;
+    };
+    auto step = [&](uint32_t d, int q, int jj) {
+        const double4 l = L[d];
+        const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
+        P = s.P;
+        M = s.M;
+        const uint32_t noP = s.bP ? oM : oP;
+        const uint32_t noM = s.bM ? oM : oP;
+        oP = noP;
+        oM = noM;
+        if (jj < 32) { wP0 |= s.bP << jj; wM0 |= s.bM << jj; }
+        else { wP1 |= s.bP << (jj - 32); wM1 |= s.bM << (jj - 32); }
+        if (jj == 63) flush(q);
+    };
+    if (g.full(k)) {
+        walk_block<true>(pk, k, g.C, step);
+    } else {
+        // partial/first block: positions outside the chunk are skipped; flush every quad
+        walk_block<false>(pk, k, g.C, [&](uint32_t d, int q, int jj) {
+            step(d, q, jj);
+        });
+        // quads whose last position was skipped were not flushed: flush all remaining
+        const int jend = g.jend(k);
+        uint32_t* o = reinterpret_cast<uint32_t*>(bpo);
+        for (int q = 0; q < 4; ++q) {
+            const int last = q * 64 + 63;
+            if (last >= jend) {
+                o[2 * q] = wP0; o[2 * q + 1] = wP1; o[8 + 2 * q] = wM0; o[8 + 2 * q + 1] = wM1;
+                wP0 = wP1 = wM0 = wM1 = 0;
+            }
+        }
+    }
+    origin[gid] = (uint8_t)(oM | (oP << 1));
+    const double2 nx = ent[k + 1];
+    if (__double_as_longlong(nx.x) != __double_as_longlong(P) ||
+        __double_as_longlong(nx.y) != __double_as_longlong(M))
+        atomicOr(status, ST_VERIFY_ENTRY);
+}
+
+// ---------------------------------------------------------------- K6: trace scan
+__device__ __forceinline__ uint32_t map_apply(uint32_t m, uint32_t x) { return (m >> x) & 1u; }
+__device__ __forceinline__ uint32_t map_compose(uint32_t f, uint32_t g) {   // f o g
+    return map_apply(f, map_apply(g, 0)) | (map_apply(f, map_apply(g, 1)) << 1);
+}
+
+__global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __restrict__ entry,
+                                                        const uint8_t* __restrict__ origin,
+                                                        uint8_t* __restrict__ endst,
+                                                        double* __restrict__ score) {
+    const int64_t c = blockIdx.x;
+    const int t = threadIdx.x;
+    const int64_t per = (g.nsb + kThreads - 1) / kThreads;
+    const int64_t b0 = t * per, b1 = min(b0 + per, g.nsb);
+    const uint8_t* og = origin + c * g.nsb;
+    const double2 fin = entry[c * (g.nsb + 1) + g.nsb];
+    const uint32_t s_end = (fin.y > fin.x) ? 0u : 1u;   // '+' first: '-' only if strictly >
+    if (t == 0 && score) score[c] = s_end ? fin.x : fin.y;
+    uint32_t F = 0x2u;
+    for (int64_t k = b0; k < b1; ++k) F = map_compose(F, og[k]);
+    __shared__ uint32_t sF[kThreads];
+    sF[t] = F;
+    __syncthreads();
+    for (int off = 1; off < kThreads; off <<= 1) {
+        uint32_t x = sF[t];
+        if (t + off < kThreads) x = map_compose(x, sF[t + off]);
+        __syncthreads();
+        sF[t] = x;
+        __syncthreads();
+    }
+    const uint32_t G = (t + 1 < kThreads) ? sF[t + 1] : 0x2u;
+    uint32_t e = map_apply(G, s_end);
+    for (int64_t k = b1 - 1; k >= b0; --k) {
+        endst[c * g.nsb + k] = (uint8_t)e;
+        e = map_apply(og[k], e);
+    }
+}
+
+// ---------------------------------------------------------------- K7: traceback
+__global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __restrict__ bp,
+                                                        const uint8_t* __restrict__ endst,
+                                                        uint32_t* __restrict__ sign_out,
+                                                        uint32_t* status) {
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gid >= g.nchunks * g.nsb) return;
+    const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
+    uint32_t wP[8], wM[8];
+    {
+        const uint4* b = bp + gid * 4;
+        uint4 x0 = b[0], x1 = b[1], x2 = b[2], x3 = b[3];
+        wP[0] = x0.x; wP[1] = x0.y; wP[2] = x0.z; wP[3] = x0.w;
+        wP[4] = x1.x; wP[5] = x1.y; wP[6] = x1.z; wP[7] = x1.w;
+        wM[0] = x2.x; wM[1] = x2.y; wM[2] = x2.z; wM[3] = x2.w;
+        wM[4] = x3.x; wM[5] = x3.y; wM[6] = x3.z; wM[7] = x3.w;
+    }
+    const int j0 = g.jfirst(k), jend = g.jend(k);
+    uint32_t s = endst[gid];
+    uint32_t out[8];
+#pragma unroll
+    for (int w = 7; w >= 0; --w) {
+        uint32_t o = 0;
+#pragma unroll
+        for (int i = 31; i >= 0; --i) {
+            const int j = w * 32 + i;
+            if (j >= j0 && j < jend) {
+                o |= s << i;
+                const uint32_t bit = ((s ? wP[w] : wM[w]) >> i) & 1u;
+                s = bit ^ 1u;
+            }
+        }
+        out[w] = o;
+    }
+    if (k == 0) out[0] |= s;   // position 0
+    else if (s != endst[gid - 1]) atomicOr(status, ST_VERIFY_CHAIN);
+    // write the block's words (positions k*256 ... k*256+255 of the chunk)
+    uint32_t* so = sign_out + c * (g.C >> 5) + k * 8;
+    const int64_t nw = (g.C + 31) >> 5;
+    if ((k + 1) * 8 <= nw) {
+        uint4* s4 = reinterpret_cast<uint4*>(so);
+        s4[0] = make_uint4(out[0], out[1], out[2], out[3]);
+        s4[1] = make_uint4(out[4], out[5], out[6], out[7]);
+    } else {
+#pragma unroll
+        for (int w = 0; w < 8; ++w)
+            if (k * 8 + w < nw) so[w] = out[w];
+    }
+}
+
+// ---------------------------------------------------------------- workspace layout
+struct VitWs {
+    int4* comp1;
+    VitPlan* plan;
+    double4* comp3;
+    double2* entry;
+    double4* gk;
+    double4* gap;
+    int32_t* barlist;
+    double2* vout;
+    int32_t* splitlist;
+    int32_t* splitcount;
+    uint4* bp;
+    uint8_t* origin;
+    uint8_t* endst;
+    uint8_t* degen;
+    size_t bytes;
+};
+
+VitWs carve(void* base, int64_t nchunks, int64_t nsb) {
+    const int64_t nt = nchunks * nsb;
+    char* p = static_cast<char*>(base);
+    size_t off = 0;
+    auto take = [&](size_t bytes) {
+        off = (off + 255) & ~size_t(255);
+        char* r = p ? p + off : nullptr;
+        off += bytes;
+        return r;
+    };
+    VitWs w;
+    w.comp1 = (int4*)take(nt * sizeof(int4));
+    w.plan = (VitPlan*)take(nt * sizeof(VitPlan));
+    w.comp3 = (double4*)take(nt * 2 * sizeof(double4));
+    w.entry = (double2*)take(nchunks * (nsb + 1) * sizeof(double2));
+    w.gk = (double4*)take(nt * sizeof(double4));
+    w.gap = (double4*)take(nt * sizeof(double4));
+    w.barlist = (int32_t*)take(nt * sizeof(int32_t));
+    w.vout = (double2*)take(nt * sizeof(double2));
+    w.splitlist = (int32_t*)take(nt * sizeof(int32_t));
+    w.splitcount = (int32_t*)take(nchunks * sizeof(int32_t));
+    w.bp = (uint4*)take(nt * 4 * sizeof(uint4));
+    w.origin = (uint8_t*)take(nt);
+    w.endst = (uint8_t*)take(nt);
+    w.degen = (uint8_t*)take(nchunks);
+    w.bytes = off + 256;
+    return w;
+}
+
+}  // namespace
+
+int64_t vit_nsb(int64_t chunk_len) { return chunk_len <= 1 ? 1 : (chunk_len + kSB - 1) / kSB; }
+
+size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len) {
+    return carve(nullptr, nchunks, vit_nsb(chunk_len)).bytes;
+}
+
+hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint32_t* packed,
+                          int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
+                          uint32_t* sign_out, double* score, uint8_t* degen_out,
+                          uint32_t* status, hipStream_t s) {
+    const int64_t nsb = vit_nsb(chunk_len);
+    VitWs w = carve(ws, nchunks, nsb);
+    if (w.bytes > ws_bytes) return hipErrorInvalidValue;
+    Geo g{nchunks, chunk_len, nsb};
+    const int64_t nt = nchunks * nsb;
+    const unsigned grid = (unsigned)((nt + kThreads - 1) / kThreads);
+    const size_t lds3 = (size_t)(vc.emax - vc.emin + 1) * 16 * sizeof(double4);
+    hipLaunchKernelGGL(k_vit_approx, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.comp1);
+    hipLaunchKernelGGL(k_vit_plan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, vc, packed, g,
+                       w.comp1, w.plan, w.degen, w.splitlist, w.splitcount);
+    hipLaunchKernelGGL(k_vit_exact, dim3(grid), dim3(kThreads), lds3, s, vc, d_vt, packed, g,
+                       w.plan, w.comp3, status);
+    hipLaunchKernelGGL(k_vit_exact_split, dim3((unsigned)nchunks), dim3(64), 0, s, vc, d_vt,
+                       packed, g, w.plan, w.splitlist, w.splitcount, w.comp3);
+    hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kThreads), 0, s, vc, packed, g,
+                       w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout);
+    hipLaunchKernelGGL(k_vit_forward, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.degen,
+                       w.entry, w.bp, w.origin, status);
+    hipLaunchKernelGGL(k_vit_tscan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, g, w.entry,
+                       w.origin, w.endst, score);
+    hipLaunchKernelGGL(k_vit_trace, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst, sign_out,
+                       status);
+    if (degen_out) {
+        hipError_t e = hipMemcpyAsync(degen_out, w.degen, nchunks, hipMemcpyDeviceToDevice, s);
+        if (e != hipSuccess) return e;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace cpg

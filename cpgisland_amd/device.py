@@ -1,0 +1,104 @@
+"""HBM-resident hot path: torch tensors as device buffers, libcpg "_d" entry points.
+
+PyTorch is plumbing here (device memory, streams, torch.distributed); every byte of the
+hot path is computed by libcpg's HIP kernels.  Buffers are int32 tensors holding the raw
+uint32 words of the packed / sign-bit layouts (include/cpg.h).
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import check, lib, ptr
+from .hmm import Context, HmmModel
+
+
+def _dp(t: torch.Tensor):
+    assert t.is_cuda and t.is_contiguous()
+    return C.c_void_p(t.data_ptr())
+
+
+def _stream():
+    return C.c_void_p(torch.cuda.current_stream().cuda_stream)
+
+
+def words16(nbases: int) -> int:
+    return (nbases + 15) // 16
+
+
+def words32(nbases: int) -> int:
+    return (nbases + 31) // 32
+
+
+def synth_host(seed: int, start: int, n: int, nthreads: int = 0):
+    """Synthetic genome slice (cpg_synth): (packed uint32[], sign uint32[])."""
+    packed = np.zeros(words16(n) + 4, np.uint32)
+    sign = np.zeros(words32(n) + 4, np.uint32)
+    check(lib.cpg_synth(C.c_uint64(seed), start, n, ptr(packed), ptr(sign), nthreads))
+    return packed, sign
+
+
+def to_device(a: np.ndarray, device) -> torch.Tensor:
+    return torch.from_numpy(np.ascontiguousarray(a).view(np.int32)).to(device)
+
+
+def count_labelled(ctx: Context, packed: torch.Tensor, sign: torch.Tensor, nbases: int,
+                   chunk_len: int = _lib.TRAIN_CHUNK, out: torch.Tensor | None = None):
+    if out is None:
+        out = torch.empty(_lib.COUNTS_I64_N, dtype=torch.int64, device=packed.device)
+    check(lib.cpg_count_labelled_d(ctx.handle, _dp(packed), _dp(sign), nbases, chunk_len,
+                                   _dp(out), _stream()))
+    return out
+
+
+def bw_estep(ctx: Context, model: HmmModel, packed: torch.Tensor, nbases: int,
+             chunk_len: int = _lib.TRAIN_CHUNK, out: torch.Tensor | None = None):
+    if out is None:
+        out = torch.empty(_lib.COUNTS_F64_N, dtype=torch.float64, device=packed.device)
+    m = model.to_struct()
+    check(lib.cpg_bw_estep_d(ctx.handle, ptr(m), _dp(packed), nbases, chunk_len, _dp(out),
+                             _stream()))
+    return out
+
+
+def viterbi(ctx: Context, model: HmmModel, packed: torch.Tensor, nbases: int,
+            chunk_len: int = _lib.DECODE_CHUNK, sign_out: torch.Tensor | None = None,
+            score: torch.Tensor | None = None):
+    nch = nbases // chunk_len
+    if sign_out is None:
+        sign_out = torch.empty(words32(nbases) + 4, dtype=torch.int32, device=packed.device)
+    if score is None:
+        score = torch.empty(max(nch, 1), dtype=torch.float64, device=packed.device)
+    m = model.to_struct()
+    check(lib.cpg_viterbi_d(ctx.handle, ptr(m), _dp(packed), nbases, chunk_len, _dp(sign_out),
+                            _dp(score), _stream()))
+    return sign_out, score
+
+
+def islands(ctx: Context, packed: torch.Tensor, sign: torch.Tensor, nbases: int,
+            chunk_len: int = _lib.DECODE_CHUNK, cap: int = 1 << 20, first_chunk: int = 0,
+            out: torch.Tensor | None = None, count: torch.Tensor | None = None):
+    """Island records (cpg_island, 32 B each) as a uint8 tensor [cap, 32] + int64 count."""
+    if out is None:
+        out = torch.empty((max(cap, 1), _lib.ISLAND_DTYPE.itemsize), dtype=torch.uint8,
+                          device=packed.device)
+    if count is None:
+        count = torch.zeros(1, dtype=torch.int64, device=packed.device)
+    check(lib.cpg_islands_at_d(ctx.handle, _dp(packed), _dp(sign), nbases, chunk_len,
+                               first_chunk, _dp(out), cap, _dp(count), _stream()))
+    return out, count
+
+
+def islands_to_numpy(out: torch.Tensor, count: torch.Tensor) -> np.ndarray:
+    n = int(count.item())
+    n = min(n, out.shape[0])
+    return out[:n].cpu().numpy().reshape(-1).view(_lib.ISLAND_DTYPE)
+
+
+def sign_to_numpy(sign: torch.Tensor, nbases: int) -> np.ndarray:
+    w = sign.cpu().numpy().view(np.uint32)
+    bits = ((w[:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1).astype(np.uint8)
+    return bits.ravel()[:nbases]

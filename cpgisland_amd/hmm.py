@@ -1,0 +1,132 @@
+"""Host-side mirror of the reference's HMM types and decode entry point.
+
+Mirrors the Mahout classes CpGIslandFinder uses (HmmModel, HmmEvaluator — imported at
+/root/reference/CpGIslandFinder.java:9-10) with the same names, argument meaning and error
+behaviour, over libcpg.so.  The compute is on the GPU (cpg_decode_states); this module
+only validates and marshals.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import _lib
+from ._lib import CpgInvalid, check, lib, ptr
+
+# state order A+ C+ G+ T+ A- C- G- T- (:182-189); emitted symbols a c g t (:191-194)
+HIDDEN_STATE_NAMES = ("A+", "C+", "G+", "T+", "A-", "C-", "G-", "T-")
+EMITTED_STATE_NAMES = ("a", "c", "g", "t")
+
+
+class HmmModel:
+    """Mahout HmmModel(transitionMatrix, emissionMatrix, initialProbabilities)."""
+
+    def __init__(self, transition, emission, initial):
+        self.a = np.ascontiguousarray(transition, dtype=np.float64).reshape(8, 8).copy()
+        self.b = np.ascontiguousarray(emission, dtype=np.float64).reshape(8, 4).copy()
+        self.pi = np.ascontiguousarray(initial, dtype=np.float64).reshape(8).copy()
+
+    # Mahout getters used at :204-222
+    def getInitialProbabilities(self):
+        return self.pi
+
+    def getTransitionMatrix(self):
+        return self.a
+
+    def getEmissionMatrix(self):
+        return self.b
+
+    def getNrOfHiddenStates(self):
+        return 8
+
+    def getNrOfOutputStates(self):
+        return 4
+
+    def to_struct(self) -> np.ndarray:
+        """cpg_model layout: pi[8] | a[8][8] | b[8][4]."""
+        return np.concatenate([self.pi, self.a.ravel(), self.b.ravel()]).astype(np.float64)
+
+    @classmethod
+    def from_struct(cls, m: np.ndarray) -> "HmmModel":
+        m = np.asarray(m, np.float64)
+        return cls(m[8:72].reshape(8, 8), m[72:104].reshape(8, 4), m[:8])
+
+    @classmethod
+    def initial(cls) -> "HmmModel":
+        """The model CpGIslandFinder.trainModel starts Baum-Welch from (:155-173)."""
+        m = np.zeros(_lib.MODEL_N, np.float64)
+        check(lib.cpg_initial_model(ptr(m)))
+        return cls.from_struct(m)
+
+    def __eq__(self, other):
+        return isinstance(other, HmmModel) and np.array_equal(self.to_struct(), other.to_struct())
+
+    def __repr__(self):
+        return f"HmmModel(pi={self.pi.tolist()})"
+
+
+class Context:
+    """One libcpg context = one device (one process per GPU)."""
+
+    def __init__(self, device: int = 0):
+        h = C.c_void_p()
+        check(lib.cpg_open(device, C.byref(h)))
+        self.handle = h
+        self.device = device
+
+    def close(self):
+        if self.handle:
+            lib.cpg_close(self.handle)
+            self.handle = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def sync(self, stream=None):
+        check(lib.cpg_sync(self.handle, stream))
+
+    def reserve(self, nbases: int):
+        check(lib.cpg_reserve(self.handle, int(nbases)))
+
+
+_default_ctx: Context | None = None
+
+
+def default_context() -> Context:
+    global _default_ctx
+    if _default_ctx is None:
+        _default_ctx = Context(0)
+    return _default_ctx
+
+
+class HmmEvaluator:
+    """Mahout HmmEvaluator — decode() is the entry point CpGIslandFinder calls (:260)."""
+
+    @staticmethod
+    def decode(model: HmmModel, observations, scaled: bool = True, ctx: Context | None = None):
+        """Most likely hidden state sequence (int32 states 0..7), bit-identical to
+        Mahout's sequential fp64 Viterbi (scaled=True).  Raises CpgInvalid (the
+        reference's ArrayIndexOutOfBounds / NegativeArraySize) on symbols outside 0..3
+        or an empty array."""
+        if not scaled:
+            raise ValueError("only scaled=True decoding is on the hot path "
+                             "(CpGIslandFinder.java:260)")
+        obs = np.ascontiguousarray(observations, dtype=np.int32)
+        if obs.ndim != 1:
+            raise CpgInvalid(_lib.CPG_E_INVALID, "observations must be 1-D")
+        ctx = ctx or default_context()
+        out = np.zeros(max(len(obs), 1), np.int32)
+        m = model.to_struct()
+        check(lib.cpg_decode_states(ctx.handle, ptr(m), ptr(obs) if len(obs) else None,
+                                    len(obs), ptr(out)))
+        return out[: len(obs)]

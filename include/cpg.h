@@ -1,0 +1,198 @@
+/*
+ * cpg.h — C-ABI of libcpg.so, the MI355X-native hot path of CpGIslandFinder.
+ *
+ * Reference: /root/reference/CpGIslandFinder.java (ErangaD/CpGIsland).  Every entry
+ * point below names the reference interface it replaces (file:line).  The reference
+ * host is Java; its drop-in binding (Panama FFM downcalls, JNI fallback) is shown in
+ * INTEGRATION.md.  No torch / HIP types appear in these signatures: plain pointers,
+ * sizes and an opaque context.  Streams are passed as `void*`: a hipStream_t, NULL
+ * meaning the HIP null stream (as in the HIP API itself).
+ *
+ * Conventions
+ *   - return 0 (CPG_OK) or a negative CPG_E_* code; no exceptions cross the ABI.
+ *     cpg_last_error() returns a thread-local message for the last failure.
+ *   - every output buffer is caller-owned.  The context owns device workspace,
+ *     pinned staging buffers and its stream.
+ *   - one call at a time per context (contexts are internally serialised); separate
+ *     contexts (one per device / process) run concurrently.
+ *   - "_d" entry points take DEVICE pointers (HBM-resident inputs, the bench path)
+ *     and are asynchronous on `stream`; call cpg_sync() to wait and collect the
+ *     context's device-side status word (set by the kernels' self checks).
+ *     Entry points without "_d" take HOST pointers, stage through pinned memory and
+ *     return after the results are in the caller's buffers.
+ *
+ * Data layout (HBM and host alike)
+ *   packed bases : uint32 words, 16 bases per word, base k at bits 2*(k%16),
+ *                  A=0 C=1 G=2 T=3 (the reference's symbol map, :114-123 / :240-249)
+ *   sign bits    : uint32 words, 32 bases per word, bit k%32; 1 = '+' (island state
+ *                  0..3), 0 = '-' (state 4..7)
+ *   model        : state order A+ C+ G+ T+ A- C- G- T- (:182-189), row-major
+ */
+#ifndef CPG_H_
+#define CPG_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CPG_ABI_VERSION 1
+
+/* status codes */
+#define CPG_OK              0
+#define CPG_E_INVALID     (-1)  /* bad argument: null pointer, size, symbol not in 0..3
+                                   (reference: ArrayIndexOutOfBounds / NegativeArraySize) */
+#define CPG_E_DEVICE      (-2)  /* HIP runtime error / no device */
+#define CPG_E_UNSUPPORTED (-3)  /* model outside the GPU path's contract (see cpg_viterbi_d) */
+#define CPG_E_CAPACITY    (-4)  /* caller's output buffer too small (*count holds the need) */
+#define CPG_E_REF_CRASH   (-5)  /* reference would throw at this input (decode ingest) */
+#define CPG_E_VERIFY      (-6)  /* a kernel's exactness self-check failed */
+
+#define CPG_TRAIN_CHUNK   65536    /* 0x10000  — CpGIslandFinder.java:130 */
+#define CPG_DECODE_CHUNK  1048576  /* 0x100000 — CpGIslandFinder.java:256 */
+
+/* HMM over the 8 hidden states x 4 symbols.  CpGIslandFinder.java:155-173 */
+typedef struct cpg_model {
+    double pi[8];
+    double a[8][8];
+    double b[8][4];
+} cpg_model;
+
+/* Baum-Welch sufficient statistics (expected counts, fp64) summed over chunks:
+ * the mapper's stripes (initial, transition row i, emission row i) behind
+ * BaumWelchDriver.runBaumWelchMR (called at CpGIslandFinder.java:200). */
+typedef struct cpg_counts_f64 {
+    double init[8];
+    double trans[8][8];
+    double emit[8][4];
+    double loglik;          /* sum over chunks of log P(chunk | model) */
+} cpg_counts_f64;
+
+/* Hard-label ("labelled") integer counts, same stripe layout + dinucleotide and
+ * mononucleotide histograms.  Build-defined. */
+typedef struct cpg_counts_i64 {
+    int64_t init[8];
+    int64_t trans[8][8];
+    int64_t emit[8][4];
+    int64_t dinuc[4][4];
+    int64_t mono[4];
+} cpg_counts_i64;
+
+#define CPG_COUNTS_I64_N 124   /* int64 fields in cpg_counts_i64 */
+#define CPG_COUNTS_F64_N 105   /* doubles in cpg_counts_f64 */
+
+/* One island record, exactly the values the reference formats at :287-288:
+ *   "%d %d %d %f %f\n", beg+chunk*0x100000+1, end+chunk*0x100000+1, islandLen,
+ *   cgcontent, oeratio   (Java int arithmetic: coordinates wrap at 2^31). */
+typedef struct cpg_island {
+    int32_t beg1;      /* 1-based start, int32-wrapped as in Java */
+    int32_t end1;      /* 1-based end (inclusive), int32-wrapped */
+    int32_t len;       /* islandLen */
+    int32_t chunk;     /* decode chunk index (0-based) */
+    double  cg;        /* (C+G)/len                         (:280) */
+    double  oe;        /* (int32)(CpG*len) / (C*G) or 0.0    (:281-283) */
+} cpg_island;
+
+typedef struct cpg_ctx cpg_ctx;
+
+/* ---- context ---------------------------------------------------------------- */
+int         cpg_open(int device, cpg_ctx** out);
+void        cpg_close(cpg_ctx* ctx);
+const char* cpg_last_error(void);
+int         cpg_abi_version(void);
+/* Pre-size the context's workspace for inputs of up to nbases bases so that the
+ * _d entry points never allocate (required before hipGraph capture). */
+int         cpg_reserve(cpg_ctx* ctx, int64_t nbases);
+/* Wait for `stream` and return the first kernel-reported status since the last
+ * cpg_sync (CPG_OK or CPG_E_VERIFY / CPG_E_UNSUPPORTED). */
+int         cpg_sync(cpg_ctx* ctx, void* stream);
+
+/* ---- host utilities (no device) ---------------------------------------------- */
+/* The reference's initial model, CpGIslandFinder.java:155-173. */
+int cpg_initial_model(cpg_model* out);
+
+/* ASCII ingest, CpGIslandFinder.java:112-145 (mode 0 = training) and :238-259
+ * (mode 1 = decode).  Maps A/a C/c G/g T/t to 0..3 and skips every other byte.
+ *   mode 0: emits whole 65,536-base chunks (tail dropped); with compat_quirks != 0 an
+ *           extra all-A chunk is emitted for every non-ACGT byte read while the base
+ *           count sits on a chunk multiple (:130-141 runs per character).
+ *   mode 1: emits whole 1,048,576-base chunks (tail never decoded, :256); with
+ *           compat_quirks != 0 returns CPG_E_REF_CRASH when the reference would call
+ *           observedSequence.get(i) on an empty list (:257-258); *nbases then holds
+ *           the bases decoded before the crash.
+ * packed: caller buffer of cap_bases/16 words; *nbases = bases written. */
+int cpg_ingest(const char* txt, size_t n, int mode, int compat_quirks,
+               uint32_t* packed, int64_t cap_bases, int64_t* nbases);
+
+/* Deterministic counter-based synthetic genome: bases
+ * [start, start+n) of the genome for `seed`, '-' background from the '-' block of the
+ * initial model, planted '+' islands (U[300,3000] long, mean gap 100 kbp).  start must
+ * be a multiple of 32.  sign_bits may be NULL.  Multithreaded (nthreads<=0: all). */
+int cpg_synth(uint64_t seed, int64_t start, int64_t n, uint32_t* packed,
+              uint32_t* sign_bits, int nthreads);
+
+/* The reducer: row-normalise init, transition rows and emission rows into a model.
+ * Replaces the MAHOUT-627 reducer + BaumWelchUtils.createHmmModel (:203). */
+int cpg_bw_normalize(const cpg_counts_f64* counts, cpg_model* out);
+/* Labelled-count M-step (same normalisation over the integer counts). */
+int cpg_counts_normalize(const cpg_counts_i64* counts, cpg_model* out);
+
+/* ---- device path: HBM-resident inputs (device pointers), async on `stream` ----- */
+
+/* Labelled counts over whole chunk_len chunks (tail dropped).  d_counts: device
+ * buffer of CPG_COUNTS_I64_N int64 (cpg_counts_i64 layout), OVERWRITTEN. */
+int cpg_count_labelled_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
+                         int64_t nbases, int64_t chunk_len, int64_t* d_counts,
+                         void* stream);
+
+/* Baum-Welch E-step (mapper) over whole chunk_len chunks; every chunk is an
+ * independent observation sequence (:130-141).  d_counts: CPG_COUNTS_F64_N doubles
+ * (cpg_counts_f64 layout), OVERWRITTEN.  Deterministic (fixed reduction order). */
+int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                   int64_t nbases, int64_t chunk_len, double* d_counts, void* stream);
+
+/* Viterbi decode, HmmEvaluator.decode(trainedModel, chunk, true) (:260), of every
+ * whole chunk_len chunk (tail not decoded, :256).  Output: the state path as sign bits
+ * (state = base + (sign ? 0 : 4)), identical to Mahout's sequential fp64 Viterbi, and
+ * the final best log-probability per chunk (d_score, may be NULL).
+ * Contract: emission rows deterministic (b[i][i%4] == 1), every a[i][j] > 0.  Else
+ * CPG_E_UNSUPPORTED.  chunk_len: a multiple of 4096. */
+int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                  int64_t nbases, int64_t chunk_len, uint32_t* d_sign_out,
+                  double* d_score, void* stream);
+
+/* Island scan + filter, CpGIslandFinder.java:262-339, over every whole chunk.
+ * d_out: capacity `cap` records; *d_count (device int64) receives the number of
+ * kept islands (written even when > cap; records beyond cap are dropped). */
+int cpg_islands_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
+                  int64_t nbases, int64_t chunk_len, cpg_island* d_out, int64_t cap,
+                  int64_t* d_count, void* stream);
+
+/* As cpg_islands_d with the chunk numbering starting at first_chunk: a shard of the
+ * genome (multi-GPU) reports the same coordinates/chunk indices as the unsharded run. */
+int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
+                     int64_t nbases, int64_t chunk_len, int64_t first_chunk,
+                     cpg_island* d_out, int64_t cap, int64_t* d_count, void* stream);
+
+/* ---- host-buffer entry points (stage through pinned memory, synchronous) ------- */
+int cpg_count_labelled(cpg_ctx* ctx, const uint32_t* packed, const uint32_t* sign,
+                       int64_t nbases, int64_t chunk_len, cpg_counts_i64* out);
+int cpg_bw_estep(cpg_ctx* ctx, const cpg_model* model, const uint32_t* packed,
+                 int64_t nbases, int64_t chunk_len, cpg_counts_f64* out);
+int cpg_viterbi(cpg_ctx* ctx, const cpg_model* model, const uint32_t* packed,
+                int64_t nbases, int64_t chunk_len, uint32_t* sign_out, double* score);
+/* Exact HmmEvaluator.decode(model, obs, true) (:260) for one observation array:
+ * obs[i] in 0..3 (else CPG_E_INVALID, the reference's ArrayIndexOutOfBounds), n >= 1.
+ * states_out[i] in 0..7. */
+int cpg_decode_states(cpg_ctx* ctx, const cpg_model* model, const int32_t* obs,
+                      int64_t n, int32_t* states_out);
+int cpg_islands(cpg_ctx* ctx, const uint32_t* packed, const uint32_t* sign,
+                int64_t nbases, int64_t chunk_len, cpg_island* out, int64_t cap,
+                int64_t* count);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CPG_H_ */

@@ -1,0 +1,349 @@
+"""GPU parity: libcpg's HIP path vs the CPU oracle on the same seeded inputs.
+
+Bit-exact for everything integer/index (labelled counts, Viterbi paths, island records) and
+for the Viterbi best score (the kernels reproduce the sequential fp64 recurrence exactly);
+Baum-Welch expected counts within a stated relative tolerance (fp64, re-associated sums).
+Every call goes through the C-ABI (libcpg.so).  PARITY UNPINNED (see oracle/cpg_oracle.h).
+"""
+import numpy as np
+import pytest
+
+from oracle import coracle as co
+from oracle import pyref as pr
+
+pytestmark = pytest.mark.gpu
+
+ESTEP_RTOL = 1e-9        # north_star: fp64 within 1e-9 relative
+TRAIN = 65536
+DECODE = 1 << 20
+
+
+@pytest.fixture(scope="module")
+def torch_dev():
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch.device("cuda:0")
+
+
+@pytest.fixture(scope="module")
+def golden():
+    import os
+    return np.load(os.path.join(os.path.dirname(__file__), "golden", "golden.npz"))
+
+
+def _model(m):
+    from cpgisland_amd import HmmModel
+    return HmmModel.from_struct(m)
+
+
+def _dev_genome(packed, sign, dev):
+    from cpgisland_amd import device as D
+    pad = np.zeros(8, np.uint32)
+    dp = D.to_device(np.concatenate([packed.astype(np.uint32), pad]), dev)
+    ds = D.to_device(np.concatenate([sign.astype(np.uint32), pad]), dev)
+    return dp, ds
+
+
+def _viterbi(ctx, m, dp, n, C):
+    import torch
+    from cpgisland_amd import device as D
+    so, sc = D.viterbi(ctx, _model(m), dp, n, C)
+    torch.cuda.synchronize()
+    ctx.sync()
+    return D.sign_to_numpy(so, n), sc.cpu().numpy()[: n // C]
+
+
+def _trained_model(m0, obs):
+    return co.normalize(co.estep(m0, obs, TRAIN))
+
+
+# ---------------------------------------------------------------- golden vectors
+def test_golden_viterbi_islands_counts(gpu_ctx, torch_dev, golden):
+    import torch
+    from cpgisland_amd import device as D
+    N = DECODE
+    dp, ds = _dev_genome(golden["synth_packed"], golden["synth_truth"], torch_dev)
+    m = golden["model_initial"]
+    sg, sc = _viterbi(gpu_ctx, m, dp, N, N)
+    assert np.array_equal(pr.pack_bits(sg), golden["viterbi_sign"])
+    assert np.array_equal(sc, golden["viterbi_score"])          # exact, not 1e-9
+    so = D.to_device(pr.pack_bits(sg), torch_dev)
+    out, cnt = D.islands(gpu_ctx, dp, so, N, N)
+    isl = D.islands_to_numpy(out, cnt)
+    assert np.array_equal(isl, golden["islands"])
+    assert "".join(co.format_island(r) for r in isl) == str(golden["islands_txt"])
+    c = D.count_labelled(gpu_ctx, dp, ds, N, TRAIN)
+    assert np.array_equal(c.cpu().numpy(), golden["counts_labelled"])
+    e = D.bw_estep(gpu_ctx, _model(m), dp, N, TRAIN)
+    torch.cuda.synchronize()
+    ref = golden["estep_counts"]
+    got = e.cpu().numpy()
+    nz = ref != 0
+    assert np.all(got[~nz] == 0)
+    assert np.max(np.abs(got[nz] - ref[nz]) / np.abs(ref[nz])) < ESTEP_RTOL
+    sg1, sc1 = _viterbi(gpu_ctx, golden["model_trained1"], dp, N, N)
+    assert np.array_equal(pr.pack_bits(sg1), golden["viterbi_sign_trained1"])
+    assert np.array_equal(sc1, golden["viterbi_score_trained1"])
+
+
+# ---------------------------------------------------------------- Viterbi
+@pytest.mark.parametrize("T", [1, 2, 3, 16, 17, 255, 256, 257, 511, 512, 513, 1000, 4097,
+                               65536, 100003])
+def test_decode_states_vs_mahout_order(gpu_ctx, T):
+    from cpgisland_amd import HmmEvaluator, HmmModel
+    rng = np.random.default_rng(T)
+    obs = rng.integers(0, 4, T).astype(np.int32)
+    m = co.initial_model()
+    st = HmmEvaluator.decode(HmmModel.from_struct(m), obs, True, ctx=gpu_ctx)
+    ref, _ = co.viterbi8(m, obs.astype(np.uint8))
+    assert np.array_equal(st, ref)
+
+
+@pytest.mark.parametrize("seed", [1, 2, 3])
+def test_viterbi_multichunk_synthetic(gpu_ctx, torch_dev, seed):
+    from cpgisland_amd import device as D
+    N = 6 * DECODE + 4321
+    packed, sign = D.synth_host(1000 + seed, 0, N)
+    obs = pr.unpack(packed, N)
+    m = co.initial_model() if seed != 3 else _trained_model(co.initial_model(), obs[:16 * TRAIN])
+    dp, _ = _dev_genome(packed, sign, torch_dev)
+    sg, sc = _viterbi(gpu_ctx, m, dp, N, DECODE)
+    states, _, score = co.decode_chunks(m, obs, DECODE)
+    nd = len(states)
+    assert np.array_equal(sg[:nd], (states < 4).astype(np.uint8))
+    assert not sg[nd:].any()                                     # tail never decoded
+    assert np.array_equal(sc, score)
+
+
+@pytest.mark.parametrize("C", [256, 4096, 65536])
+def test_viterbi_small_chunks(gpu_ctx, torch_dev, C):
+    rng = np.random.default_rng(C)
+    N = 40 * C + 100
+    obs = rng.integers(0, 4, N).astype(np.uint8)
+    m = co.initial_model()
+    dp, _ = _dev_genome(pr.pack(obs), np.zeros(N // 32 + 1, np.uint32), torch_dev)
+    sg, sc = _viterbi(gpu_ctx, m, dp, N, C)
+    for c in range(N // C):
+        s2, best = co.viterbi2(m, obs[c * C:(c + 1) * C])
+        assert np.array_equal(sg[c * C:(c + 1) * C], s2), c
+        assert sc[c] == best
+
+
+def test_viterbi_adversarial_inputs(gpu_ctx, torch_dev):
+    m = co.initial_model()
+    n = DECODE
+    cases = {
+        "cg": np.tile(np.array([1, 2], np.uint8), n // 2),
+        "at": np.tile(np.array([0, 3], np.uint8), n // 2),
+        "allA": np.zeros(n, np.uint8),
+        "allC": np.ones(n, np.uint8),
+        "blocks": np.repeat(np.random.default_rng(0).integers(0, 4, n // 4096), 4096)
+                  .astype(np.uint8),
+    }
+    for name, obs in cases.items():
+        dp, _ = _dev_genome(pr.pack(obs), np.zeros(n // 32, np.uint32), torch_dev)
+        sg, sc = _viterbi(gpu_ctx, m, dp, n, n)
+        s2, best = co.viterbi2(m, obs)
+        assert np.array_equal(sg, s2), name
+        assert sc[0] == best, name
+
+
+def test_viterbi_extreme_models(gpu_ctx, torch_dev):
+    """Tiny transition probabilities (large |log a|: other fixed-point scale and binade
+    range), pi with zeros, and the degenerate pi = 0 for both live states."""
+    from cpgisland_amd import HmmEvaluator, HmmModel
+    rng = np.random.default_rng(4)
+    n = 3 * 4096
+    obs = rng.integers(0, 4, n).astype(np.uint8)
+    pi, a, b = co.model_split(co.initial_model())
+    a2 = a.copy()
+    a2[:4, 4:] = 1e-12
+    a2[4:, :4] = 1e-9
+    a2 /= a2.sum(axis=1, keepdims=True)
+    for m in (co.model_flat(pi, a2, b),
+              co.model_flat(np.array([0, .25, .25, .25, 0, .1, .1, .05]), a, b)):
+        dp, _ = _dev_genome(pr.pack(obs), np.zeros(n // 32 + 1, np.uint32), torch_dev)
+        sg, sc = _viterbi(gpu_ctx, m, dp, n, 4096)
+        for c in range(3):
+            st, best = co.viterbi8(m, obs[c * 4096:(c + 1) * 4096])
+            assert np.array_equal(sg[c * 4096:(c + 1) * 4096], (st < 4).astype(np.uint8))
+            assert sc[c] == best
+    # degenerate: pi[o0+] = pi[o0-] = 0
+    mdeg = co.model_flat(np.array([0, .25, .25, .25, 0, .1, .1, .05]), a, b)
+    o = obs[:5000].astype(np.int32)
+    o[0] = 0
+    st = HmmEvaluator.decode(HmmModel.from_struct(mdeg), o, ctx=gpu_ctx)
+    ref, _ = co.viterbi8(mdeg, o.astype(np.uint8))
+    assert np.array_equal(st, ref)
+    st1 = HmmEvaluator.decode(HmmModel.from_struct(mdeg), o[:1], ctx=gpu_ctx)
+    ref1, _ = co.viterbi8(mdeg, o[:1].astype(np.uint8))
+    assert np.array_equal(st1, ref1)
+
+
+def test_viterbi_score_is_path_score_full_size(gpu_ctx, torch_dev):
+    """Size-independent property at the C2 size (46 Mbp, 43 chunks): the reported best
+    score equals the log-probability of the decoded path (within 1e-9 relative), and every
+    chunk's kernel self-check (block exit == next block entry, bitwise) passed."""
+    from cpgisland_amd import device as D
+    N = 46_000_000
+    packed, sign = D.synth_host(20251016, 0, N)
+    m = co.initial_model()
+    dp, _ = _dev_genome(packed, sign, torch_dev)
+    sg, sc = _viterbi(gpu_ctx, m, dp, N, DECODE)
+    obs = pr.unpack(packed, N)
+    L = np.log(m[8:72].reshape(8, 8))
+    for c in range(0, N // DECODE, 7):
+        o = obs[c * DECODE:(c + 1) * DECODE].astype(np.int64)
+        s = o + np.where(sg[c * DECODE:(c + 1) * DECODE] != 0, 0, 4)
+        v = np.log(m[s[0]]) + L[s[:-1], s[1:]].sum()
+        assert abs(v - sc[c]) <= 1e-9 * abs(sc[c])
+    # one full chunk bitwise against the oracle
+    c = 21
+    s2, best = co.viterbi2(m, obs[c * DECODE:(c + 1) * DECODE])
+    assert np.array_equal(sg[c * DECODE:(c + 1) * DECODE], s2) and sc[c] == best
+
+
+def test_decode_errors(gpu_ctx):
+    from cpgisland_amd import CpgError, CpgInvalid, HmmEvaluator, HmmModel
+    from cpgisland_amd import _lib
+    m = HmmModel.initial()
+    with pytest.raises(CpgInvalid):
+        HmmEvaluator.decode(m, np.array([0, 1, 4], np.int32), ctx=gpu_ctx)
+    with pytest.raises(CpgInvalid):
+        HmmEvaluator.decode(m, np.array([], np.int32), ctx=gpu_ctx)
+    bad = HmmModel.initial()
+    bad.b[0] = [0.9, 0.1, 0, 0]
+    with pytest.raises(CpgError) as e:
+        HmmEvaluator.decode(bad, np.array([0, 1, 2], np.int32), ctx=gpu_ctx)
+    assert e.value.code == _lib.CPG_E_UNSUPPORTED
+
+
+# ---------------------------------------------------------------- labelled counts
+@pytest.mark.parametrize("C", [256, 4096, 65536])
+@pytest.mark.parametrize("kind", ["random", "synth", "plus", "minus"])
+def test_counts_bit_exact(gpu_ctx, torch_dev, C, kind):
+    from cpgisland_amd import device as D
+    rng = np.random.default_rng(C)
+    N = 37 * C + 123
+    if kind == "synth":
+        packed, sign = D.synth_host(77, 0, N)
+        obs, sg = pr.unpack(packed, N), pr.unpack_bits(sign, N)
+    else:
+        obs = rng.integers(0, 4, N).astype(np.uint8)
+        sg = {"random": (rng.random(N) < 0.5), "plus": np.ones(N),
+              "minus": np.zeros(N)}[kind].astype(np.uint8)
+    dp, ds = _dev_genome(pr.pack(obs), pr.pack_bits(sg), torch_dev)
+    got = D.count_labelled(gpu_ctx, dp, ds, N, C).cpu().numpy()
+    assert np.array_equal(got, co.count_labelled(obs, sg, C))
+
+
+def test_counts_full_size_properties(gpu_ctx, torch_dev):
+    """C2 size: totals are exact identities of the chunk geometry; invariant under sharding."""
+    from cpgisland_amd import device as D
+    N = 46_000_000
+    packed, sign = D.synth_host(5, 0, N)
+    dp, ds = _dev_genome(packed, sign, torch_dev)
+    full = D.count_labelled(gpu_ctx, dp, ds, N, TRAIN).cpu().numpy()
+    nch = N // TRAIN
+    assert full[:8].sum() == nch and full[8:72].sum() == nch * (TRAIN - 1)
+    assert full[120:124].sum() == nch * TRAIN and full[104:120].sum() == nch * (TRAIN - 1)
+    # sharded in 4 contiguous pieces of whole chunks: the sum is identical
+    per = (nch // 4) * TRAIN
+    acc = np.zeros(124, np.int64)
+    for r in range(4):
+        n_r = per if r < 3 else (nch - 3 * nch // 4) * TRAIN
+        acc += D.count_labelled(gpu_ctx, dp[r * per // 16:], ds[r * per // 32:], n_r,
+                                TRAIN).cpu().numpy()
+    assert np.array_equal(acc, full)
+
+
+# ---------------------------------------------------------------- islands
+def test_islands_random_states_vs_oracle(gpu_ctx, torch_dev):
+    from cpgisland_amd import device as D
+    rng = np.random.default_rng(12)
+    C = 4096
+    nch = 64
+    N = nch * C
+    states = np.concatenate([np.resize(_rand_states(rng), C) for _ in range(nch)])
+    obs = (states % 4).astype(np.uint8)
+    sg = (states < 4).astype(np.uint8)
+    dp, ds = _dev_genome(pr.pack(obs), pr.pack_bits(sg), torch_dev)
+    for first in (0, 2048 * 256 - 3):      # the second crosses chunk*C = 2^31 (int wrap)
+        out, cnt = D.islands(gpu_ctx, dp, ds, N, C, first_chunk=first)
+        got = D.islands_to_numpy(out, cnt)
+        exp = np.concatenate([co.islands(states[c * C:(c + 1) * C], first + c)
+                              for c in range(nch)])
+        assert len(exp) > 100
+        assert np.array_equal(got, exp)
+
+
+def _rand_states(rng):
+    out = []
+    while len(out) < 4096:
+        plus = rng.random() < 0.4
+        L = int(rng.integers(1, 60))
+        b = rng.choice(4, L, p=[0.15, 0.35, 0.35, 0.15] if plus else [0.3, 0.2, 0.2, 0.3])
+        out += [int(x) + (0 if plus else 4) for x in b]
+    return np.array(out, np.int32)
+
+
+def test_islands_long_overflow_island(gpu_ctx, torch_dev):
+    from cpgisland_amd import device as D
+    C = 1 << 17
+    st = np.full(C, 6, np.int32)
+    st[10:10 + 70000] = np.resize(np.array([1, 2], np.int32), 70000)   # cg*len overflows
+    st[80000:81000] = np.resize(np.array([1, 2, 0], np.int32), 1000)
+    st[90000:90010] = [3, 3, 3, 1, 4, 2, 2, 1, 2, 2]                     # stale atC
+    st[90010:90020] = [4, 4, 4, 0, 2, 4, 4, 4, 4, 4]
+    dp, ds = _dev_genome(pr.pack((st % 4).astype(np.uint8)),
+                         pr.pack_bits((st < 4).astype(np.uint8)), torch_dev)
+    out, cnt = D.islands(gpu_ctx, dp, ds, C, C)
+    assert np.array_equal(D.islands_to_numpy(out, cnt), co.islands(st, 0))
+
+
+def test_islands_capacity(gpu_ctx, torch_dev, golden):
+    from cpgisland_amd import device as D
+    N = DECODE
+    dp, _ = _dev_genome(golden["synth_packed"], golden["synth_truth"], torch_dev)
+    so = D.to_device(golden["viterbi_sign"], torch_dev)
+    out, cnt = D.islands(gpu_ctx, dp, so, N, N, cap=3)
+    assert int(cnt.item()) == len(golden["islands"])
+    assert np.array_equal(out[:3].cpu().numpy().reshape(-1).view(co.ISLAND_DTYPE),
+                          golden["islands"][:3])
+
+
+# ---------------------------------------------------------------- E-step
+@pytest.mark.parametrize("C", [4096, 16384, 65536])
+def test_estep_tolerance_and_determinism(gpu_ctx, torch_dev, C):
+    import torch
+    from cpgisland_amd import device as D
+    N = 9 * C + 77
+    packed, sign = D.synth_host(31 + C, 0, N)
+    obs = pr.unpack(packed, N)
+    m = co.initial_model()
+    dp, _ = _dev_genome(packed, sign, torch_dev)
+    e1 = D.bw_estep(gpu_ctx, _model(m), dp, N, C).cpu().numpy()
+    e2 = D.bw_estep(gpu_ctx, _model(m), dp, N, C).cpu().numpy()
+    torch.cuda.synchronize()
+    assert np.array_equal(e1, e2)                                 # deterministic
+    ref = co.estep(m, obs, C)
+    nz = ref != 0
+    assert np.all(e1[~nz] == 0)
+    assert np.max(np.abs(e1[nz] - ref[nz]) / np.abs(ref[nz])) < ESTEP_RTOL
+    # the M-step of the GPU counts is the oracle's model to the same tolerance
+    assert np.allclose(co.normalize(e1), co.normalize(ref), rtol=ESTEP_RTOL, atol=0)
+
+
+def test_estep_trained_model_iteration(gpu_ctx, torch_dev):
+    """Two Baum-Welch iterations on the GPU track the oracle's (model after iteration 2)."""
+    from cpgisland_amd import device as D
+    N = 24 * TRAIN
+    packed, sign = D.synth_host(99, 0, N)
+    obs = pr.unpack(packed, N)
+    dp, _ = _dev_genome(packed, sign, torch_dev)
+    mg = mo = co.initial_model()
+    for _ in range(2):
+        mg = co.normalize(D.bw_estep(gpu_ctx, _model(mg), dp, N, TRAIN).cpu().numpy())
+        mo = co.normalize(co.estep(mo, obs, TRAIN))
+    assert np.allclose(mg, mo, rtol=1e-8, atol=0)
