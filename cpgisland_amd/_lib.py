@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libcpg.so")
+LIB_PATH = os.environ.get("CPG_LIB_OVERRIDE") or os.path.join(_HERE, "libcpg.so")  # override: dev ablations only
 
 CPG_OK = 0
 CPG_E_INVALID = -1

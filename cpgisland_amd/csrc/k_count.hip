@@ -151,7 +151,7 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
         uint64_t acc = 0;
 #pragma unroll
         for (int w = 0; w < kCountThreads / 64; ++w) acc += wsum[w][threadIdx.x];
-        slab[(int64_t)blockIdx.x * kRaw + threadIdx.x] = acc;
+        slab[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = acc;   // counter-major
     }
 }
 
@@ -167,21 +167,36 @@ __global__ void k_count_init(const uint32_t* __restrict__ packed,
     first_state[c] = (uint32_t)(b + (s ? 0 : 4));
 }
 
-__global__ __launch_bounds__(256) void k_count_final(const uint64_t* __restrict__ slab,
-                                                     int nrows,
-                                                     const uint32_t* __restrict__ first_state,
-                                                     int64_t nchunks,
-                                                     int64_t* __restrict__ out) {
-    __shared__ uint64_t raw[kRaw];
-    __shared__ uint64_t initc[8][256];
+// one workgroup per counter: fixed-order tree sum of that counter's per-workgroup partials
+__global__ __launch_bounds__(256) void k_count_reduce(const uint64_t* __restrict__ slab,
+                                                      int nrows, uint64_t* __restrict__ raw) {
+    __shared__ uint64_t s[256];
     const int t = threadIdx.x;
-    if (t < 64) {
-        uint64_t acc = 0;
-        for (int r = 0; r < nrows; ++r) acc += slab[(int64_t)r * kRaw + t];
-        raw[t] = acc;
+    const uint64_t* row = slab + (int64_t)blockIdx.x * nrows;
+    uint64_t acc = 0;
+    for (int r = t; r < nrows; r += 256) acc += row[r];
+    s[t] = acc;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) s[t] += s[t + o];
+        __syncthreads();
     }
-    uint64_t ic[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int64_t c = t; c < nchunks; c += 256) ic[first_state[c] & 7u]++;
+    if (t == 0) raw[blockIdx.x] = s[0];
+}
+
+__global__ __launch_bounds__(256) void k_count_final(const uint64_t* __restrict__ raw_in,
+                                                     const uint32_t* __restrict__ first_state,
+                                                     int64_t nchunks, int64_t* __restrict__ out) {
+    __shared__ uint64_t raw[kRaw];
+    __shared__ uint32_t initc[8][256];
+    const int t = threadIdx.x;
+    if (t < 64) raw[t] = raw_in[t];
+    uint32_t ic[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    for (int64_t c = t; c < nchunks; c += 256) {
+        const uint32_t fs = first_state[c];
+#pragma unroll
+        for (int k = 0; k < 8; ++k) ic[k] += (fs == (uint32_t)k);
+    }
 #pragma unroll
     for (int k = 0; k < 8; ++k) initc[k][t] = ic[k];
     __syncthreads();
@@ -191,32 +206,40 @@ __global__ __launch_bounds__(256) void k_count_final(const uint64_t* __restrict_
         raw[64 + t] = acc;
     }
     __syncthreads();
-    if (t != 0) return;
-    // cpg_counts_i64 layout: init[8] trans[8][8] emit[8][4] dinuc[4][4] mono[4]
-    int64_t* init = out;
-    int64_t* trans = out + 8;
-    int64_t* emit = out + 72;
-    int64_t* dinuc = out + 104;
-    int64_t* mono = out + 120;
-    for (int i = 0; i < 124; ++i) out[i] = 0;
-    for (int s = 0; s < 8; ++s) init[s] = (int64_t)raw[64 + s];
-    for (int p = 0; p < 4; ++p)
-        for (int b = 0; b < 4; ++b) {
-            int d = p * 4 + b;
-            int64_t tt = (int64_t)raw[d], ppv = (int64_t)raw[16 + d],
-                    pmv = (int64_t)raw[32 + d], mpv = (int64_t)raw[48 + d];
-            trans[p * 8 + b] = ppv;
-            trans[p * 8 + b + 4] = pmv;
-            trans[(p + 4) * 8 + b] = mpv;
-            trans[(p + 4) * 8 + b + 4] = tt - ppv - pmv - mpv;
-            dinuc[d] = tt;
+    if (t >= 124) return;
+    // cpg_counts_i64 layout: init[8] trans[8][8] emit[8][4] dinuc[4][4] mono[4]; one
+    // output word per thread
+    int64_t v = 0;
+    if (t < 8) {
+        v = (int64_t)raw[64 + t];
+    } else if (t < 72) {
+        const int i = (t - 8) >> 3, j = (t - 8) & 7;      // trans[i][j]
+        const int d = (i & 3) * 4 + (j & 3), si = i >> 2, sj = j >> 2;
+        const int64_t tt = (int64_t)raw[d], ppv = (int64_t)raw[16 + d],
+                      pmv = (int64_t)raw[32 + d], mpv = (int64_t)raw[48 + d];
+        v = si == 0 ? (sj == 0 ? ppv : pmv) : (sj == 0 ? mpv : tt - ppv - pmv - mpv);
+    } else if (t < 104) {
+        const int s = (t - 72) >> 2, k = (t - 72) & 3;     // emit[s][k]
+        if (k == (s & 3)) {
+            v = (int64_t)raw[64 + s];
+            for (int r = 0; r < 8; ++r) {
+                const int d = (r & 3) * 4 + (s & 3), si = r >> 2, sj = s >> 2;
+                const int64_t tt = (int64_t)raw[d], ppv = (int64_t)raw[16 + d],
+                              pmv = (int64_t)raw[32 + d], mpv = (int64_t)raw[48 + d];
+                v += si == 0 ? (sj == 0 ? ppv : pmv) : (sj == 0 ? mpv : tt - ppv - pmv - mpv);
+            }
         }
-    for (int s = 0; s < 8; ++s) {
-        int64_t col = init[s];
-        for (int r = 0; r < 8; ++r) col += trans[r * 8 + s];
-        emit[s * 4 + (s & 3)] = col;
-        mono[s & 3] += col;
+    } else if (t < 120) {
+        const int p = (t - 104) >> 2, b = (t - 104) & 3;    // dinuc[p][b]
+        v = (int64_t)raw[p * 4 + b];
+    } else {
+        const int b = t - 120;                               // mono[b] = sum_p dinuc + inits
+        // every base at a chunk position > 0 is the cur base of one transition; position 0
+        // is counted by init
+        for (int p = 0; p < 4; ++p) v += (int64_t)raw[p * 4 + b];
+        v += (int64_t)raw[64 + b] + (int64_t)raw[64 + b + 4];
     }
+    out[t] = v;
 }
 
 }  // namespace
@@ -228,21 +251,25 @@ hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nc
     if ((int64_t)grid * kCountThreads > nblk) grid = (int)((nblk + kCountThreads - 1) / kCountThreads);
     if (grid < 1) grid = 1;
     uint64_t* slab = ws;
-    uint32_t* first_state = (uint32_t*)(ws + (size_t)1024 * kRaw);
-    if (nblk > 0)
+    uint64_t* raw = ws + (size_t)1024 * kRaw;
+    uint32_t* first_state = (uint32_t*)(raw + 128);
+    if (nblk > 0) {
         hipLaunchKernelGGL(k_count_main, dim3(grid), dim3(kCountThreads), 0, s,
                            (const uint4*)packed, (const uint2*)sign, packed, sign, nblk,
                            chunk_len / 64, slab);
+        hipLaunchKernelGGL(k_count_reduce, dim3(64), dim3(256), 0, s, slab, grid, raw);
+    } else {
+        hipMemsetAsync(raw, 0, 64 * sizeof(uint64_t), s);
+    }
     if (nchunks > 0)
         hipLaunchKernelGGL(k_count_init, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0,
                            s, packed, sign, nchunks, chunk_len, first_state);
-    hipLaunchKernelGGL(k_count_final, dim3(1), dim3(256), 0, s, slab, nblk > 0 ? grid : 0,
-                       first_state, nchunks, out);
+    hipLaunchKernelGGL(k_count_final, dim3(1), dim3(256), 0, s, raw, first_state, nchunks, out);
     return hipGetLastError();
 }
 
 size_t count_ws_bytes(int64_t nchunks) {
-    return (size_t)1024 * kRaw * 8 + (size_t)(nchunks + 1) * 4;
+    return (size_t)1024 * kRaw * 8 + 128 * 8 + (size_t)(nchunks + 1) * 4;
 }
 
 }  // namespace cpg

@@ -11,7 +11,9 @@
 //      vector leaving every lane's 64 positions;
 //   3. each lane walks its positions in 16-position mini-blocks: forward alphas kept in
 //      registers, backward betas from 3 checkpoints, posterior pair marginals xi_p(i,j)
-//      = alpha_{p-1}(i) M_p(i,j) beta_p(j) / Z_p accumulated into per-wave LDS bins.
+//      = alpha_{p-1}(i) M_p(i,j) beta_p(j) / Z_p accumulated into per-wave LDS bins in
+//      unsigned fixed point (2^-47, round to nearest) with integer LDS atomics: exact,
+//      order-independent sums (measured: fp64 LDS atomics were 2x the integer ones).
 // Posteriors are normalised per position, so the scaling scheme (exact powers of two here,
 // reciprocal of the sum in the reference) changes results only at rounding level: parity
 // with the oracle is by tolerance (tests: 1e-9 relative).  Emission counts follow exactly
@@ -60,11 +62,58 @@ __device__ __forceinline__ void vnorm(double& x, double& y) {
     }
 }
 
-__device__ __forceinline__ uint32_t dinuc_lds(const uint32_t* sw, int p) {   // p >= 1
-    const uint32_t b = (sw[p >> 4] >> ((p & 15) * 2)) & 3u;
-    const int q = p - 1;
-    const uint32_t a = (sw[q >> 4] >> ((q & 15) * 2)) & 3u;
-    return a | (b << 2);
+// 1/z to full fp64 precision: hardware reciprocal + two Newton steps (explicit fma)
+__device__ __forceinline__ double rcp_nr(double z) {
+    double r = __builtin_amdgcn_rcp(z);
+    double e = fma(-z, r, 1.0);
+    r = fma(r, e, r);
+    e = fma(-z, r, 1.0);
+    return fma(r, e, r);
+}
+
+// posterior in [0,1] -> unsigned fixed point 2^-47 (round to nearest): a chunk's 65,536
+// positions sum below 2^63, integer LDS atomics are exact and order-independent
+constexpr double kFix = 140737488355328.0;        // 2^47
+__device__ __forceinline__ unsigned long long to_fixed(double x) {
+    const double y = rint(x * kFix);                 // exact scaling, then round
+    const double hi = floor(y * 0x1.0p-32);
+    const uint32_t h = (uint32_t)hi;
+    const uint32_t l = (uint32_t)fma(-hi, 4294967296.0, y);
+    return ((unsigned long long)h << 32) | l;
+}
+
+// the lane's 64 dinucleotide codes (prev | cur << 2), 8 per word, read once from HBM
+struct Codes {
+    uint32_t w[8];
+    // the 16 codes of mini-block m (runtime m: a select chain, no register indexing)
+    __device__ __forceinline__ uint64_t mb(int m) const {
+        const uint32_t lo = m == 0 ? w[0] : m == 1 ? w[2] : m == 2 ? w[4] : w[6];
+        const uint32_t hi = m == 0 ? w[1] : m == 1 ? w[3] : m == 2 ? w[5] : w[7];
+        return ((uint64_t)hi << 32) | lo;
+    }
+};
+__device__ __forceinline__ uint32_t code_at(uint64_t mb, int i) {   // i compile-time
+    return (uint32_t)(mb >> (4 * i)) & 15u;
+}
+__device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int t) {
+    const uint4 v = *reinterpret_cast<const uint4*>(pk + 4 * t);
+    const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
+    uint32_t prev = t > 0 ? pk[4 * t - 1] : 0u;
+    Codes c;
+#pragma unroll
+    for (int k = 0; k < 8; ++k) c.w[k] = 0u;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+#pragma unroll
+        for (int i = 0; i < 16; ++i) {
+            const int j = r * 16 + i;
+            const uint32_t d = (i == 0) ? (__builtin_amdgcn_alignbit(ww[r], prev, 30) & 15u)
+                                        : ((ww[r] >> (2 * i - 2)) & 15u);
+            c.w[j >> 3] |= d << ((j & 7) * 4);
+        }
+        prev = ww[r];
+    }
+    return c;
 }
 
 __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
@@ -72,21 +121,23 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
                                                      int64_t C, double* __restrict__ slab) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
-    const int nwords = (int)(C / 16);
-    uint32_t* sw = reinterpret_cast<uint32_t*>(smem);                          // C/16 words
-    double4* T = reinterpret_cast<double4*>(smem + ((nwords * 4 + 15) & ~15));  // 16
-    double* bins = reinterpret_cast<double*>(T + 16);                            // [waves][64]
-    Mat* sm = reinterpret_cast<Mat*>(bins + (kET / 64) * 64);                    // [nl]
+    const int nw = nl / 64;                // waves
+    // conflict-free constant tables: 16 x 16 B each = one 256-B bank row
+    double2* TA = reinterpret_cast<double2*>(smem);          // (M(+,+), M(+,-))
+    double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
+    auto* bins = reinterpret_cast<unsigned long long*>(TB + 16);   // [wave][4 replicas][64]
+    Mat* sm = reinterpret_cast<Mat*>(bins + nw * 4 * 64);     // [nl] (scan; then checkpoints)
     const int t = threadIdx.x;
+    const int lane = t & 63;
     const int64_t c = blockIdx.x;
     const uint32_t* pk = packed + c * (C / 16);
-    for (int i = t; i < nwords; i += nl) sw[i] = pk[i];
     if (t < 16) {
         const int p = t & 3, b = t >> 2;
-        T[t] = make_double4(model.a[p][b], model.a[p][b + 4], model.a[p + 4][b],
-                            model.a[p + 4][b + 4]);
+        TA[t] = make_double2(model.a[p][b], model.a[p][b + 4]);
+        TB[t] = make_double2(model.a[p + 4][b], model.a[p + 4][b + 4]);
     }
-    for (int i = t; i < (kET / 64) * 64; i += nl) bins[i] = 0.0;
+    for (int i = t; i < nw * 4 * 64; i += nl) bins[i] = 0ull;
+    const Codes cd = lane_codes(pk, t);
     __syncthreads();
 
     constexpr int L = kLanePos;            // 64 positions per lane
@@ -94,14 +145,20 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     const int p0 = t * L;
     // 1. lane product of M_p over its positions (position 0 carries no matrix)
     Mat P = mid();
-    for (int p = (t == 0 ? 1 : p0); p < p0 + L; ++p) {
-        const double4 m = T[dinuc_lds(sw, p)];
-        Mat r{P.a * m.x + P.b * m.z, P.a * m.y + P.b * m.w, P.c * m.x + P.d * m.z,
-              P.c * m.y + P.d * m.w, P.e};
-        P = r;
-        if ((p & 7) == 7) mnorm(P);
+#pragma unroll 1
+    for (int m = 0; m < NMB; ++m) {
+        const uint64_t cm = cd.mb(m);
+#pragma unroll
+        for (int i = 0; i < kMB; ++i) {
+            if (t == 0 && m == 0 && i == 0) continue;
+            const uint32_t d = code_at(cm, i);
+            const double2 ma = TA[d], mb = TB[d];
+            Mat r{P.a * ma.x + P.b * mb.x, P.a * ma.y + P.b * mb.y, P.c * ma.x + P.d * mb.x,
+                  P.c * ma.y + P.d * mb.y, P.e};
+            P = r;
+            if ((i & 7) == 7) mnorm(P);
+        }
     }
-    mnorm(P);
     // 2a. inclusive prefix (Hillis-Steele)
     sm[t] = P;
     __syncthreads();
@@ -112,8 +169,8 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         sm[t] = x;
         __syncthreads();
     }
-    const uint32_t o0 = sw[0] & 3u;
-    const double fa = model.pi[o0], fb = model.pi[o0 + 4];   // alpha_0 (b = 1 on the live states)
+    const uint32_t o0 = pk[0] & 3u;
+    const double fa = model.pi[o0], fb = model.pi[o0 + 4];   // alpha_0 (b = 1 when live)
     double loglik = 0.0;
     if (t == nl - 1) {
         const Mat A = sm[nl - 1];
@@ -147,47 +204,51 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         bM = B.c + B.d;
     }
     vnorm(bP, bM);
-
-    // 3a. backward checkpoints: beta at the last position of each mini-block, kept in LDS
-    //     ([m][lane] double2, aliasing the scan buffer: conflict-free 16-B rows)
     __syncthreads();
+
+    // 3a. backward checkpoints: beta at the last position of each mini-block ([m][lane] in
+    //     LDS, aliasing the scan buffer: 16-B rows, conflict-free)
     double2* ck = reinterpret_cast<double2*>(sm);
     {
         double xP = bP, xM = bM;
+#pragma unroll 1
         for (int m = NMB - 1; m >= 0; --m) {
             ck[m * nl + t] = make_double2(xP, xM);
             if (m == 0) break;
-            for (int p = p0 + m * kMB + kMB - 1; p >= p0 + m * kMB; --p) {
-                const double4 mm = T[dinuc_lds(sw, p)];
-                const double nP = mm.x * xP + mm.y * xM, nM = mm.z * xP + mm.w * xM;
+            const uint64_t cm = cd.mb(m);
+#pragma unroll
+            for (int i = kMB - 1; i >= 0; --i) {
+                const uint32_t d = code_at(cm, i);
+                const double2 ma = TA[d], mb = TB[d];
+                const double nP = ma.x * xP + ma.y * xM, nM = mb.x * xP + mb.y * xM;
                 xP = nP;
                 xM = nM;
-                vnorm(xP, xM);
+                if ((i & 3) == 0) vnorm(xP, xM);
             }
         }
     }
     // 3b. mini-blocks: forward alphas in registers, then backward with xi accumulation
-    double* wb = bins + (t >> 6) * 64;
+    unsigned long long* wb = bins + ((t >> 6) * 4 + (lane >> 4)) * 64;   // 16-lane replica
     double g0P = 0.0, g0M = 0.0;
     double bfP = aP, bfM = aM;   // alpha at the position before the mini-block
-#pragma unroll
+#pragma unroll 1
     for (int m = 0; m < NMB; ++m) {
-        const int q0 = p0 + m * kMB;
+        const uint64_t cm = cd.mb(m);
         double alP[kMB], alM[kMB];
         double xP = bfP, xM = bfM;
 #pragma unroll
         for (int i = 0; i < kMB; ++i) {
-            const int p = q0 + i;
-            if (p == 0) {   // alpha_0 itself (lane 0, mini-block 0)
+            if (t == 0 && m == 0 && i == 0) {   // alpha_0 itself
                 alP[i] = xP;
                 alM[i] = xM;
                 continue;
             }
-            const double4 mm = T[dinuc_lds(sw, p)];
-            const double nP = xP * mm.x + xM * mm.z, nM = xP * mm.y + xM * mm.w;
+            const uint32_t d = code_at(cm, i);
+            const double2 ma = TA[d], mb = TB[d];
+            const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
             xP = nP;
             xM = nM;
-            vnorm(xP, xM);
+            if ((i & 3) == 3) vnorm(xP, xM);
             alP[i] = xP;
             alM[i] = xM;
         }
@@ -195,8 +256,7 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         double yP = cz.x, yM = cz.y;
 #pragma unroll
         for (int i = kMB - 1; i >= 0; --i) {
-            const int p = q0 + i;
-            if (p == 0) {   // gamma_0 -> init counts
+            if (t == 0 && m == 0 && i == 0) {   // gamma_0 -> init counts
                 const double gp = alP[0] * yP, gm = alM[0] * yM, z = gp + gm;
                 g0P = gp / z;
                 g0M = gm / z;
@@ -204,74 +264,87 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             }
             const double uP = i > 0 ? alP[i - 1] : bfP;
             const double uM = i > 0 ? alM[i - 1] : bfM;
-            const uint32_t d = dinuc_lds(sw, p);
-            const double4 mm = T[d];
-            const double x00 = uP * mm.x * yP, x01 = uP * mm.y * yM, x10 = uM * mm.z * yP,
-                         x11 = uM * mm.w * yM;
-            const double rz = 1.0 / ((x00 + x01) + (x10 + x11));
-            double* bq = wb + d * 4;
-            atomicAdd(bq + 0, x00 * rz);
-            atomicAdd(bq + 1, x01 * rz);
-            atomicAdd(bq + 2, x10 * rz);
-            atomicAdd(bq + 3, x11 * rz);
-            const double nP = mm.x * yP + mm.y * yM, nM = mm.z * yP + mm.w * yM;
+            const uint32_t d = code_at(cm, i);
+            const double2 ma = TA[d], mb = TB[d];
+            const double x00 = uP * ma.x * yP, x01 = uP * ma.y * yM, x10 = uM * mb.x * yP,
+                         x11 = uM * mb.y * yM;
+            const double rz = rcp_nr((x00 + x01) + (x10 + x11));
+            unsigned long long* bu = wb + d * 4;
+            atomicAdd(bu + 0, to_fixed(x00 * rz));
+            atomicAdd(bu + 1, to_fixed(x01 * rz));
+            atomicAdd(bu + 2, to_fixed(x10 * rz));
+            atomicAdd(bu + 3, to_fixed(x11 * rz));
+            const double nP = ma.x * yP + ma.y * yM, nM = mb.x * yP + mb.y * yM;
             yP = nP;
             yM = nM;
-            vnorm(yP, yM);
+            if ((i & 3) == 0) vnorm(yP, yM);
         }
         bfP = alP[kMB - 1];
         bfM = alM[kMB - 1];
     }
     __syncthreads();
-    double* sl = slab + c * kSlab;
+    // slab is counter-major: [kSlab][nchunks]
+    const int64_t nch = gridDim.x;
     if (t < 64) {
-        double s = 0.0;
-        for (int w = 0; w < nl / 64; ++w) s += bins[w * 64 + t];
-        sl[t] = s;
+        unsigned long long s = 0;
+        for (int r = 0; r < nw * 4; ++r) s += bins[r * 64 + t];
+        slab[t * nch + c] = (double)s * (1.0 / kFix);
     }
     if (t == 0) {
-        for (int i = 0; i < 8; ++i) sl[64 + i] = 0.0;
-        sl[64 + o0] = g0P;
-        sl[64 + o0 + 4] = g0M;
+        for (int i = 0; i < 8; ++i) slab[(64 + i) * nch + c] = 0.0;
+        slab[(64 + o0) * nch + c] = g0P;
+        slab[(64 + o0 + 4) * nch + c] = g0M;
     }
-    if (t == nl - 1) sl[72] = loglik;
+    if (t == nl - 1) slab[72 * nch + c] = loglik;
 }
 
-__global__ __launch_bounds__(128) void k_estep_final(const double* __restrict__ slab,
-                                                     int64_t nchunks, double* __restrict__ out) {
-    __shared__ double v[kSlab];
+// one workgroup per counter: fixed-order tree sum over chunks (deterministic)
+__global__ __launch_bounds__(256) void k_estep_reduce(const double* __restrict__ slab,
+                                                      int64_t nchunks, double* __restrict__ v) {
+    __shared__ double s[256];
     const int t = threadIdx.x;
-    if (t < kSlab) {
-        double s = 0.0;
-        for (int64_t c = 0; c < nchunks; ++c) s += slab[c * kSlab + t];
-        v[t] = s;
-    }
+    const double* row = slab + (int64_t)blockIdx.x * nchunks;
+    double acc = 0.0;
+    for (int64_t c = t; c < nchunks; c += 256) acc += row[c];
+    s[t] = acc;
     __syncthreads();
-    if (t != 0) return;
-    // cpg_counts_f64: init[8] trans[8][8] emit[8][4] loglik
-    double* init = out;
-    double* trans = out + 8;
-    double* emit = out + 72;
-    for (int i = 0; i < 105; ++i) out[i] = 0.0;
-    for (int s = 0; s < 8; ++s) init[s] = v[64 + s];
-    for (int d = 0; d < 16; ++d) {
-        const int p = d & 3, b = d >> 2;
-        trans[p * 8 + b] = v[d * 4 + 0];
-        trans[p * 8 + b + 4] = v[d * 4 + 1];
-        trans[(p + 4) * 8 + b] = v[d * 4 + 2];
-        trans[(p + 4) * 8 + b + 4] = v[d * 4 + 3];
+    for (int o = 128; o > 0; o >>= 1) {
+        if (t < o) s[t] += s[t + o];
+        __syncthreads();
     }
-    for (int j = 0; j < 8; ++j) {
-        double col = init[j];
-        for (int i = 0; i < 8; ++i) col += trans[i * 8 + j];
-        emit[j * 4 + (j & 3)] = col;
+    if (t == 0) v[blockIdx.x] = s[0];
+}
+
+__global__ __launch_bounds__(128) void k_estep_final(const double* __restrict__ v,
+                                                     double* __restrict__ out) {
+    // cpg_counts_f64: init[8] trans[8][8] emit[8][4] loglik; one output per thread
+    const int t = threadIdx.x;
+    if (t >= 105) return;
+    double r = 0.0;
+    if (t < 8) {
+        r = v[64 + t];
+    } else if (t < 72) {
+        const int i = (t - 8) >> 3, j = (t - 8) & 7;
+        const int d = (i & 3) | ((j & 3) << 2);
+        r = v[d * 4 + (i >> 2) * 2 + (j >> 2)];
+    } else if (t < 104) {
+        const int jj = (t - 72) >> 2, k = (t - 72) & 3;
+        if (k == (jj & 3)) {                       // emit[j] = init[j] + sum_i trans[i][j]
+            r = v[64 + jj];
+            for (int i = 0; i < 8; ++i) {
+                const int d = (i & 3) | ((jj & 3) << 2);
+                r += v[d * 4 + (i >> 2) * 2 + (jj >> 2)];
+            }
+        }
+    } else {
+        r = v[72];
     }
-    out[104] = v[72];
+    out[t] = r;
 }
 
 }  // namespace
 
-size_t estep_ws_bytes(int64_t nchunks, int64_t) { return (size_t)(nchunks + 1) * kSlab * 8 + 1024; }
+size_t estep_ws_bytes(int64_t nchunks, int64_t) { return (size_t)(nchunks + 1) * kSlab * 8 + 4096; }
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t C, void* ws, size_t ws_bytes, double* out, hipStream_t s) {
@@ -279,13 +352,17 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
     if (C % 4096 || C > (int64_t)kET * kLanePos) return hipErrorInvalidValue;
     const int lanes = (int)(C / kLanePos);
     double* slab = static_cast<double*>(ws);
-    const size_t lds = (size_t)((C / 16 * 4 + 15) & ~15) + 16 * sizeof(double4) +
-                       (kET / 64) * 64 * sizeof(double) +
+    const size_t lds = 32 * sizeof(double2) + (size_t)(lanes / 64) * 4 * 64 * sizeof(double) +
                        std::max(lanes * sizeof(Mat), (size_t)lanes * (kLanePos / 16) * 16);
     if (nchunks > 0)
         hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
                            packed, C, slab);
-    hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(128), 0, s, slab, nchunks, out);
+    double* v = slab + (size_t)(nchunks + 1) * kSlab;
+    if (nchunks > 0)
+        hipLaunchKernelGGL(k_estep_reduce, dim3(kSlab), dim3(256), 0, s, slab, nchunks, v);
+    else if (hipMemsetAsync(v, 0, kSlab * sizeof(double), s) != hipSuccess)
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(128), 0, s, v, out);
     return hipGetLastError();
 }
 

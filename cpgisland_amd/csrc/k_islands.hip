@@ -56,6 +56,10 @@ __device__ __forceinline__ WordMasks word_masks(const uint32_t* __restrict__ pk,
     return m;
 }
 
+struct Cnt5 {
+    int32_t c, g, cg, st, cl;
+};
+
 struct IslWs {
     int32_t* Cp;        // per word exclusive prefix (chunk-local)
     int32_t* Gp;
@@ -67,6 +71,7 @@ struct IslWs {
     int32_t* ncloses;
     int64_t* nkept;
     int64_t* off;
+    void* tiles;        // Cnt5 per (chunk, tile)
     size_t bytes;
 };
 
@@ -91,71 +96,115 @@ IslWs carve_isl(void* base, int64_t nchunks, int64_t C) {
     w.ncloses = (int32_t*)take(nchunks * 4);
     w.nkept = (int64_t*)take(nchunks * 8);
     w.off = (int64_t*)take((nchunks + 1) * 8);
+    w.tiles = take(nchunks * ((nw + 1023) / 1024) * 20 + 16);
     w.bytes = o + 256;
     return w;
 }
 
-// block-wide exclusive scan of 5 int32 counters (kIT threads)
-struct Cnt5 {
-    int32_t c, g, cg, st, cl;
-};
 
-__global__ __launch_bounds__(kIT) void k_isl_a(const uint32_t* packed, const uint32_t* sign,
-                                               int64_t C, IslWs ws) {
-    const int64_t c = blockIdx.x;
+// Pass A, tiled: a tile = 1024 sign words (32,768 positions) of one chunk, 4 words per lane.
+constexpr int kTileW = 1024;
+constexpr int kAT = 256;
+
+__device__ __forceinline__ Cnt5 cnt_of(const WordMasks& m) {
+    return Cnt5{(int32_t)__popc(m.C), (int32_t)__popc(m.G), (int32_t)__popc(m.CG),
+                (int32_t)__popc(m.start), (int32_t)__popc(m.close)};
+}
+__device__ __forceinline__ Cnt5 cadd(Cnt5 a, const Cnt5& b) {
+    a.c += b.c; a.g += b.g; a.cg += b.cg; a.st += b.st; a.cl += b.cl;
+    return a;
+}
+
+// block-wide exclusive scan of one Cnt5 per lane; returns (exclusive, total)
+__device__ __forceinline__ Cnt5 block_scan(Cnt5 v, Cnt5* sb, Cnt5& total) {
     const int t = threadIdx.x;
-    const int64_t nw = C / 32;   // C % 32 == 0 (checked on host)
+    sb[t] = v;
+    __syncthreads();
+    for (int off = 1; off < kAT; off <<= 1) {
+        Cnt5 x = sb[t];
+        if (t >= off) x = cadd(x, sb[t - off]);
+        __syncthreads();
+        sb[t] = x;
+        __syncthreads();
+    }
+    total = sb[kAT - 1];
+    const Cnt5 e = t > 0 ? sb[t - 1] : Cnt5{0, 0, 0, 0, 0};
+    __syncthreads();
+    return e;
+}
+
+// A1: tile totals
+__global__ __launch_bounds__(kAT) void k_isl_a1(const uint32_t* packed, const uint32_t* sign,
+                                               int64_t C, int ntiles, Cnt5* __restrict__ tiles) {
+    const int64_t c = blockIdx.x / ntiles;
+    const int tile = blockIdx.x - (int)c * ntiles;
+    const int64_t nw = C / 32;
     const uint32_t* pk = packed + c * (C / 16);
     const uint32_t* sg = sign + c * nw;
-    const int64_t per = (nw + kIT - 1) / kIT;
-    const int64_t w0 = min((int64_t)t * per, nw), w1 = min(w0 + per, nw);
     Cnt5 s{0, 0, 0, 0, 0};
-    for (int64_t w = w0; w < w1; ++w) {
-        const WordMasks m = word_masks(pk, sg, w);
-        s.c += __popc(m.C);
-        s.g += __popc(m.G);
-        s.cg += __popc(m.CG);
-        s.st += __popc(m.start);
-        s.cl += __popc(m.close);
+    const int64_t w0 = (int64_t)tile * kTileW + threadIdx.x * 4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        if (w0 + i < nw) s = cadd(s, cnt_of(word_masks(pk, sg, w0 + i)));
+    __shared__ Cnt5 sb[kAT];
+    Cnt5 tot;
+    block_scan(s, sb, tot);
+    if (threadIdx.x == 0) tiles[blockIdx.x] = tot;
+}
+
+// A2: per chunk, exclusive scan of its tile totals (in place) + run counts
+__global__ __launch_bounds__(64) void k_isl_a2(int ntiles, Cnt5* __restrict__ tiles, IslWs ws) {
+    const int64_t c = blockIdx.x;
+    if (threadIdx.x != 0) return;
+    Cnt5 acc{0, 0, 0, 0, 0};
+    for (int i = 0; i < ntiles; ++i) {
+        const Cnt5 x = tiles[c * ntiles + i];
+        tiles[c * ntiles + i] = acc;
+        acc = cadd(acc, x);
     }
-    __shared__ Cnt5 sb[kIT];
-    sb[t] = s;
-    __syncthreads();
-    for (int off = 1; off < kIT; off <<= 1) {
-        Cnt5 v = sb[t];
-        if (t >= off) {
-            const Cnt5 u = sb[t - off];
-            v.c += u.c; v.g += u.g; v.cg += u.cg; v.st += u.st; v.cl += u.cl;
+    ws.nruns[c] = acc.st;
+    ws.ncloses[c] = acc.cl;
+}
+
+// A3: word prefixes and run boundaries
+__global__ __launch_bounds__(kAT) void k_isl_a3(const uint32_t* packed, const uint32_t* sign,
+                                               int64_t C, int ntiles,
+                                               const Cnt5* __restrict__ tiles, IslWs ws) {
+    const int64_t c = blockIdx.x / ntiles;
+    const int tile = blockIdx.x - (int)c * ntiles;
+    const int64_t nw = C / 32, maxr = C / 2 + 1;
+    const uint32_t* pk = packed + c * (C / 16);
+    const uint32_t* sg = sign + c * nw;
+    const int64_t w0 = (int64_t)tile * kTileW + threadIdx.x * 4;
+    WordMasks m[4];
+    Cnt5 s{0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        if (w0 + i < nw) {
+            m[i] = word_masks(pk, sg, w0 + i);
+            s = cadd(s, cnt_of(m[i]));
         }
-        __syncthreads();
-        sb[t] = v;
-        __syncthreads();
     }
-    Cnt5 e = t > 0 ? sb[t - 1] : Cnt5{0, 0, 0, 0, 0};
-    const int64_t maxr = C / 2 + 1;
+    __shared__ Cnt5 sb[kAT];
+    Cnt5 tot;
+    Cnt5 e = cadd(block_scan(s, sb, tot), tiles[blockIdx.x]);
     int32_t* Cp = ws.Cp + c * nw;
     int32_t* Gp = ws.Gp + c * nw;
     int32_t* CGp = ws.CGp + c * nw;
     uint32_t* st = ws.starts + c * maxr;
     uint32_t* cl = ws.closes + c * maxr;
-    for (int64_t w = w0; w < w1; ++w) {
-        const WordMasks m = word_masks(pk, sg, w);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int64_t w = w0 + i;
+        if (w >= nw) break;
         Cp[w] = e.c;
         Gp[w] = e.g;
         CGp[w] = e.cg;
-        e.c += __popc(m.C);
-        e.g += __popc(m.G);
-        e.cg += __popc(m.CG);
-        for (uint32_t x = m.start; x; x &= x - 1) st[e.st++] = (uint32_t)(w * 32 + __ffs(x) - 1);
-        for (uint32_t x = m.close; x; x &= x - 1) cl[e.cl++] = (uint32_t)(w * 32 + __ffs(x) - 1);
-    }
-    if (t == kIT - 1) {
-        ws.nruns[c] = sb[kIT - 1].st;
-        ws.ncloses[c] = sb[kIT - 1].cl;
-#ifdef CPG_DEBUG_ISL
-        printf("isl_a chunk %d: starts %d closes %d C %d G %d CG %d\n", (int)c, sb[kIT - 1].st,
-               sb[kIT - 1].cl, sb[kIT - 1].c, sb[kIT - 1].g, sb[kIT - 1].cg);
-#endif
+        e.c += __popc(m[i].C);
+        e.g += __popc(m[i].G);
+        e.cg += __popc(m[i].CG);
+        for (uint32_t x = m[i].start; x; x &= x - 1) st[e.st++] = (uint32_t)(w * 32 + __ffs(x) - 1);
+        for (uint32_t x = m[i].close; x; x &= x - 1) cl[e.cl++] = (uint32_t)(w * 32 + __ffs(x) - 1);
     }
 }
 
@@ -347,8 +396,13 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
     IslWs ws = carve_isl(wsp, nchunks, chunk_len);
     if (ws.bytes > ws_bytes) return hipErrorInvalidValue;
     if (nchunks == 0) return hipMemsetAsync(count, 0, sizeof(int64_t), s);
-    hipLaunchKernelGGL(k_isl_a, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
-                       chunk_len, ws);
+    const int ntiles = (int)((chunk_len / 32 + kTileW - 1) / kTileW);
+    Cnt5* tiles = static_cast<Cnt5*>(ws.tiles);
+    hipLaunchKernelGGL(k_isl_a1, dim3((unsigned)(nchunks * ntiles)), dim3(kAT), 0, s, packed,
+                       sign, chunk_len, ntiles, tiles);
+    hipLaunchKernelGGL(k_isl_a2, dim3((unsigned)nchunks), dim3(64), 0, s, ntiles, tiles, ws);
+    hipLaunchKernelGGL(k_isl_a3, dim3((unsigned)(nchunks * ntiles)), dim3(kAT), 0, s, packed,
+                       sign, chunk_len, ntiles, tiles, ws);
     hipLaunchKernelGGL(k_isl_b, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
                        chunk_len, ws);
     hipLaunchKernelGGL(k_isl_c, dim3(1), dim3(kIT), 0, s, nchunks, ws, count);

@@ -197,34 +197,26 @@ __device__ __forceinline__ bool binade_ok(const VitConsts& vc, int e) {
     return e >= vc.emin && e <= vc.emax && !((vc.tie_mask >> e) & 1ull);
 }
 
-__global__ __launch_bounds__(kThreads) void k_vit_plan(VitConsts vc, const uint32_t* packed,
-                                                       Geo g, const int4* __restrict__ comp,
-                                                       VitPlan* __restrict__ plan,
-                                                       uint8_t* __restrict__ degen,
-                                                       int32_t* __restrict__ splitlist,
-                                                       int32_t* __restrict__ splitcount) {
+// K2a: per chunk (1024 lanes): scan of the K1 composites -> approximate value entering
+// every block (fixed point, int64); aent[nsb] = value after the last block.
+constexpr int kScanT = 1024;
+__global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_t* packed, Geo g,
+                                                     const int4* __restrict__ comp,
+                                                     longlong2* __restrict__ aent,
+                                                     uint8_t* __restrict__ degen) {
     const int64_t c = blockIdx.x;
     const int t = threadIdx.x;
     const uint32_t* pk = chunk_ptr(packed, g, c);
     const int4* cc = comp + c * g.nsb;
-    VitPlan* pl = plan + c * g.nsb;
-    __shared__ CI buf[kThreads];
-    __shared__ int4 Q[16];
-    __shared__ int nsplit;
-    if (t < 16) Q[t] = make_int4(vc.Q[t][0], vc.Q[t][1], vc.Q[t][2], vc.Q[t][3]);
-    if (t == 0) nsplit = 0;
-    const int64_t per = (g.nsb + kThreads - 1) / kThreads;
-    const int64_t b0 = t * per, b1 = min(b0 + per, g.nsb);
-
+    longlong2* ae = aent + c * (g.nsb + 1);
+    __shared__ CI buf[kScanT];
+    const int64_t per = (g.nsb + kScanT - 1) / kScanT;
+    const int64_t b0 = min((int64_t)t * per, g.nsb), b1 = min(b0 + per, g.nsb);
     const uint32_t o0 = base_at(pk, 0);
     const double lp = vc.logpi[o0], lm = vc.logpi[o0 + 4];
     const bool dg = !(lp > -INFINITY) && !(lm > -INFINITY);
     if (t == 0) degen[c] = dg ? 1 : 0;
-    if (dg) {
-        for (int64_t k = b0; k < b1; ++k) pl[k] = VitPlan{PLAN_DEGEN, 0, 0, 0, 0, 0};
-        if (t == 0) splitcount[c] = 0;
-        return;
-    }
+    if (dg) return;
     CI prod = ci_id();
     for (int64_t k = b0; k < b1; ++k) {
         const int4 x = cc[k];
@@ -232,81 +224,63 @@ __global__ __launch_bounds__(kThreads) void k_vit_plan(VitConsts vc, const uint3
     }
     buf[t] = prod;
     __syncthreads();
-    for (int off = 1; off < kThreads; off <<= 1) {
+    for (int off = 1; off < kScanT; off <<= 1) {
         CI v = buf[t];
         if (t >= off) v = ci_mul(buf[t - off], v);
         __syncthreads();
         buf[t] = v;
         __syncthreads();
     }
-    const CI excl = t > 0 ? buf[t - 1] : ci_id();
     const int f = vc.qshift;
-    const double S = ldexp(1.0, f), invS = 1.0 / S;
-    const double epsc = vc.eps + invS;   // candidates: + constant rounding
     int64_t P = fix_of(lp, f), M = fix_of(lm, f);
-    ci_apply(P, M, excl);
+    if (t > 0) ci_apply(P, M, buf[t - 1]);
     for (int64_t k = b0; k < b1; ++k) {
-        const int64_t eP = P, eM = M;
+        ae[k] = make_longlong2(P, M);
         const int4 x = cc[k];
         ci_apply(P, M, CI{x.x, x.y, x.z, x.w});
-        VitPlan p{PLAN_SEQ, 0, 0, 0, 0, 0};
-        const int j0 = g.jfirst(k), jend = g.jend(k);
-        if (k > 0 && jend > j0) {
-            const double hi = (double)mx(eP, eM) * invS + vc.eps;
-            const double lo = (double)mx(P, M) * invS - vc.eps - vc.spread;
-            if (hi < 0.0) {
-                const int e = ilogb(-hi);
-                if (binade_ok(vc, e) && lo > -ldexp(1.0, e + 1)) {
-                    p = VitPlan{PLAN_REGULAR, (int8_t)e, 0, 0, (uint16_t)jend, (uint16_t)jend};
-                } else {
-                    // locate the crossing with the approximate recurrence
-                    const bool okA = binade_ok(vc, e), okB = binade_ok(vc, e + 1);
-                    const double loA = -ldexp(1.0, e + 1), hiA = -ldexp(1.0, e);
-                    const double loB = -ldexp(1.0, e + 2), hiB = loA;
-                    int t1 = -1, lastbad = j0 - 1;
-                    int64_t aP = eP, aM = eM;
-                    auto scan = [&](uint32_t d, int q, int jj) {
-                        const int j = q * 64 + jj;
-                        const int4 qq = Q[d];
-                        const int64_t c0 = aP + qq.x, c1 = aM + qq.y, c2 = aP + qq.z,
-                                      c3 = aM + qq.w;
-                        const double vmax = (double)mx(aP, aM) * invS + epsc;
-                        const double vmin =
-                            (double)min(min(min(c0, c1), min(c2, c3)), min(aP, aM)) * invS - epsc;
-                        const bool regA = okA && vmax <= hiA && vmin > loA;
-                        const bool regB = okB && vmax <= hiB && vmin > loB;
-                        if (!regA && t1 < 0) t1 = j;
-                        if (!regB) lastbad = j;
-                        aP = mx(c0, c1);
-                        aM = mx(c2, c3);
-                    };
-                    if (g.full(k)) walk_block<true>(pk, k, g.C, scan);
-                    else walk_block<false>(pk, k, g.C, scan);
-                    if (t1 < 0) t1 = jend;
-                    int t2 = lastbad + 1;
-                    if (!okA) t1 = j0;
-                    if (!okB) t2 = jend;
-                    if (t2 < t1) t2 = t1;
-                    if (!(t1 == j0 && t2 == jend))
-                        p = VitPlan{PLAN_SPLIT, (int8_t)e, (int8_t)(e + 1), 0, (uint16_t)t1,
-                                    (uint16_t)t2};
-                }
-            }
-        }
-        pl[k] = p;
-        if (p.type == PLAN_SPLIT) {
-            int slot = atomicAdd(&nsplit, 1);
-            splitlist[c * g.nsb + slot] = (int32_t)k;
-        }
     }
-    __syncthreads();
-    if (t == 0) splitcount[c] = nsplit;
+    if (b1 == g.nsb && b0 < b1) ae[g.nsb] = make_longlong2(P, M);
+}
+
+// K2b: one lane per block: REGULAR (inside one binade) or irregular (listed for K3b);
+// block 0 is always sequential; DEGEN chunks skip everything
+__global__ __launch_bounds__(kThreads) void k_vit_classify(
+    VitConsts vc, Geo g, const longlong2* __restrict__ aent, const uint8_t* __restrict__ degen,
+    VitPlan* __restrict__ plan, int32_t* __restrict__ irrlist, int32_t* __restrict__ irrcount) {
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gid >= g.nchunks * g.nsb) return;
+    const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
+    if (degen[c]) {
+        plan[gid] = VitPlan{PLAN_DEGEN, 0, 0, 0, 0, 0};
+        return;
+    }
+    const longlong2 en = aent[c * (g.nsb + 1) + k], ex = aent[c * (g.nsb + 1) + k + 1];
+    const double invS = ldexp(1.0, -vc.qshift);
+    VitPlan p{PLAN_SEQ, 0, 0, 0, 0, 0};
+    const int j0 = g.jfirst(k), jend = g.jend(k);
+    bool irregular = false;
+    if (k > 0 && jend > j0) {
+        const double hi = (double)mx(en.x, en.y) * invS + vc.eps;
+        const double lo = (double)mx(ex.x, ex.y) * invS - vc.eps - vc.spread;
+        const int e = hi < 0.0 ? ilogb(-hi) : -1;
+        if (e >= 0 && binade_ok(vc, e) && lo > -ldexp(1.0, e + 1))
+            p = VitPlan{PLAN_REGULAR, (int8_t)e, 0, 0, (uint16_t)jend, (uint16_t)jend};
+        else
+            irregular = hi < 0.0;
+    }
+    plan[gid] = p;
+    if (irregular) {
+        const int slot = atomicAdd(irrcount + c, 1);
+        irrlist[c * g.nsb + slot] = (int32_t)k;
+    }
 }
 
 // ---------------------------------------------------------------- K3: exact composites
 // comp3 per block: pre (4 doubles) | post (4 doubles)
+// largest finite magnitude (the identity's -inf entries carry no rounding)
+__device__ __forceinline__ double fin(double x) { return x > -INFINITY ? fabs(x) : 0.0; }
 __device__ __forceinline__ double c64_absmax(const C64& c) {
-    return fmax(fmax(fabs(c.pp), fabs(c.pm)), fmax(fabs(c.mp), fabs(c.mm)));
+    return fmax(fmax(fin(c.pp), fin(c.pm)), fmax(fin(c.mp), fin(c.mm)));
 }
 __device__ __forceinline__ bool c64_exact(const C64& c, int e, double spread) {
     return c64_absmax(c) + spread < ldexp(1.0, e + 1);
@@ -317,11 +291,15 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
                                                         VitPlan* __restrict__ plan,
                                                         double4* __restrict__ comp3,
                                                         uint32_t* status) {
-    extern __shared__ __attribute__((aligned(16))) double4 sLe[];   // [e - emin][16]
+    // [e - emin][16] x 16 B per half: each half-table of a binade is one 256-B bank row
+    extern __shared__ __attribute__((aligned(16))) double2 sLe[];
     const int nb = vc.emax - vc.emin + 1;
+    double2* sA = sLe;
+    double2* sB = sLe + nb * 16;
     for (int i = threadIdx.x; i < nb * 16; i += kThreads) {
         const double* s = vt->Le[vc.emin + i / 16][i % 16];
-        sLe[i] = make_double4(s[0], s[1], s[2], s[3]);
+        sA[i] = make_double2(s[0], s[1]);
+        sB[i] = make_double2(s[2], s[3]);
     }
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -330,11 +308,12 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     if (p.type != PLAN_REGULAR) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     const uint32_t* pk = chunk_ptr(packed, g, c);
-    const double4* tab = sLe + (p.e_pre - vc.emin) * 16;
+    const double2* ta = sA + (p.e_pre - vc.emin) * 16;
+    const double2* tb = sB + (p.e_pre - vc.emin) * 16;
     C64 acc = c64_id();
     auto step = [&](uint32_t d, int, int) {
-        const double4 l = tab[d];
-        c64_step(acc, l.x, l.y, l.z, l.w);
+        const double2 a = ta[d], b = tb[d];
+        c64_step(acc, a.x, a.y, b.x, b.y);
     };
     if (g.full(k)) walk_block<true>(pk, k, g.C, step);
     else walk_block<false>(pk, k, g.C, step);
@@ -346,37 +325,161 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     comp3[gid * 2 + 1] = make_double4(0.0, -INFINITY, -INFINITY, 0.0);
 }
 
-// split blocks: pre composite on [jfirst, t1) at e_pre, post composite on [t2, jend) at e_post
-__global__ __launch_bounds__(64) void k_vit_exact_split(VitConsts vc, const VitTables* vt,
-                                                        const uint32_t* packed, Geo g,
-                                                        VitPlan* __restrict__ plan,
-                                                        const int32_t* __restrict__ splitlist,
-                                                        const int32_t* __restrict__ splitcount,
-                                                        double4* __restrict__ comp3) {
+// K3b: irregular blocks, 16 lanes per block (lane i owns positions [16i, 16i+16)):
+//   locate — fixed-point composites of the 16-position pieces, a 16-lane scan of them from
+//            the block's approximate entry, then every lane checks its own 16 steps:
+//            t1 = first step outside binade e, t2 = 1 + last step outside binade e+1;
+//   split  — exact composites of the steps before t1 (binade e) and from t2 on (binade
+//            e+1), per lane, multiplied in order by a 16-lane scan (exact max-plus).
+// Result: SPLIT (pre composite, window [t1, t2), post composite) or SEQ.
+__device__ __forceinline__ CI shfl_ci(const CI& x, int src) {
+    return {__shfl(x.pp, src), __shfl(x.pm, src), __shfl(x.mp, src), __shfl(x.mm, src)};
+}
+__device__ __forceinline__ C64 shfl_c64(const C64& x, int src) {
+    return {__shfl(x.pp, src), __shfl(x.pm, src), __shfl(x.mp, src), __shfl(x.mm, src)};
+}
+
+// the 16 steps of piece i of block k: f(d, j) with j the position offset in the block
+template <class F>
+__device__ __forceinline__ void walk_piece(const uint32_t* __restrict__ pk, int64_t k, int i,
+                                           int j0, int jend, F&& f) {
+    const int64_t wbase = k * kSBWords + i;
+    const uint32_t w = (k * kSB + i * 16 < (int64_t)jend + k * kSB) ? pk[wbase] : 0u;
+    const uint32_t prev = (k > 0 || i > 0) ? pk[wbase - 1] : 0u;
+#pragma unroll
+    for (int s = 0; s < 16; ++s) {
+        const int j = i * 16 + s;
+        const uint32_t d = (s == 0) ? (__builtin_amdgcn_alignbit(w, prev, 30) & 15u)
+                                    : ((w >> (2 * s - 2)) & 15u);
+        if (j >= j0 && j < jend) f(d, j);
+    }
+}
+
+__global__ __launch_bounds__(256) void k_vit_irregular(VitConsts vc, const VitTables* vt,
+                                                      const uint32_t* packed, Geo g,
+                                                      const longlong2* __restrict__ aent,
+                                                      VitPlan* __restrict__ plan,
+                                                      const int32_t* __restrict__ irrlist,
+                                                      const int32_t* __restrict__ irrcount,
+                                                      double4* __restrict__ comp3) {
+    extern __shared__ __attribute__((aligned(16))) double2 sLe[];   // [A|B][e - emin][16]
+    __shared__ int4 Q[16];
     const int64_t c = blockIdx.x;
-    const int n = splitcount[c];
+    const int n = irrcount[c];
+    if (n == 0) return;
+    const int nb = vc.emax - vc.emin + 1;
+    double2* sA = sLe;
+    double2* sB = sLe + nb * 16;
+    for (int i = threadIdx.x; i < nb * 16; i += 256) {
+        const double* s = vt->Le[vc.emin + i / 16][i % 16];
+        sA[i] = make_double2(s[0], s[1]);
+        sB[i] = make_double2(s[2], s[3]);
+    }
+    if (threadIdx.x < 16)
+        Q[threadIdx.x] = make_int4(vc.Q[threadIdx.x][0], vc.Q[threadIdx.x][1],
+                                   vc.Q[threadIdx.x][2], vc.Q[threadIdx.x][3]);
+    __syncthreads();
     const uint32_t* pk = chunk_ptr(packed, g, c);
-    for (int i = threadIdx.x; i < n; i += 64) {
-        const int64_t k = splitlist[c * g.nsb + i];
+    const int lane = threadIdx.x & 63;
+    const int gi = lane & 15;                       // piece index within the block
+    const int gbase = (threadIdx.x & ~15);          // first thread of the 16-lane group
+    const int gsrc = lane & ~15;                    // first lane of the group in the wave
+    const int group = threadIdx.x >> 4;             // 16 groups per workgroup
+    for (int it = group; it < n; it += 16) {
+        (void)gbase;
+        const int64_t k = irrlist[c * g.nsb + it];
         const int64_t gid = c * g.nsb + k;
-        VitPlan p = plan[gid];
-        const double(*ta)[4] = vt->Le[p.e_pre];
-        const double(*tb)[4] = vt->Le[p.e_post];
-        C64 pre = c64_id(), post = c64_id();
-        const int t1 = p.t1, t2 = p.t2;
-        auto step = [&](uint32_t d, int q, int jj) {
-            const int j = q * 64 + jj;
-            if (j < t1) c64_step(pre, ta[d][0], ta[d][1], ta[d][2], ta[d][3]);
-            else if (j >= t2) c64_step(post, tb[d][0], tb[d][1], tb[d][2], tb[d][3]);
-        };
-        if (g.full(k)) walk_block<true>(pk, k, g.C, step);
-        else walk_block<false>(pk, k, g.C, step);
-        if (!c64_exact(pre, p.e_pre, vc.spread) || !c64_exact(post, p.e_post, vc.spread)) {
-            plan[gid].type = PLAN_SEQ;
-            continue;
+        const int j0 = g.jfirst(k), jend = g.jend(k);
+        const longlong2 en = aent[c * (g.nsb + 1) + k];
+        const double invS = ldexp(1.0, -vc.qshift);
+        const double epsc = vc.eps + invS;
+        const double hi = (double)mx(en.x, en.y) * invS + vc.eps;
+        const int e = ilogb(-hi);
+        const bool okA = binade_ok(vc, e), okB = binade_ok(vc, e + 1);
+        const double S = ldexp(1.0, vc.qshift);
+        // binade conditions as fixed-point thresholds (see K2b)
+        const int64_t HA = (int64_t)floor((-ldexp(1.0, e) - epsc) * S);
+        const int64_t LA = (int64_t)floor((-ldexp(1.0, e + 1) + epsc) * S);
+        const int64_t HB = (int64_t)floor((-ldexp(1.0, e + 1) - epsc) * S);
+        const int64_t LB = (int64_t)floor((-ldexp(1.0, e + 2) + epsc) * S);
+        // locate: piece composite -> group scan -> entry of the piece
+        CI pc = ci_id();
+        walk_piece(pk, k, gi, j0, jend, [&](uint32_t d, int) {
+            const int4 q = Q[d];
+            pc = CI{cl(mx(pc.pp + q.x, pc.pm + q.y)), cl(mx(pc.pp + q.z, pc.pm + q.w)),
+                    cl(mx(pc.mp + q.x, pc.mm + q.y)), cl(mx(pc.mp + q.z, pc.mm + q.w))};
+        });
+        CI sc = pc;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const CI o = shfl_ci(sc, gsrc + ((gi - off) & 15));
+            if (gi >= off) sc = ci_mul(o, sc);
         }
-        comp3[gid * 2] = make_double4(pre.pp, pre.pm, pre.mp, pre.mm);
-        comp3[gid * 2 + 1] = make_double4(post.pp, post.pm, post.mp, post.mm);
+        const CI ex = shfl_ci(sc, gsrc + ((gi - 1) & 15));
+        int64_t aP = en.x, aM = en.y;
+        if (gi > 0) ci_apply(aP, aM, ex);
+        int t1 = 1 << 20, lastbad = -1;
+        walk_piece(pk, k, gi, j0, jend, [&](uint32_t d, int j) {
+            const int4 q = Q[d];
+            const int64_t c0 = aP + q.x, c1 = aM + q.y, c2 = aP + q.z, c3 = aM + q.w;
+            const int64_t vmax = mx(aP, aM);
+            const int64_t vmin = min(min(min(c0, c1), min(c2, c3)), min(aP, aM));
+            const bool regA = okA && vmax <= HA && vmin > LA;
+            const bool regB = okB && vmax <= HB && vmin > LB;
+            if (!regA && j < t1) t1 = j;
+            if (!regB) lastbad = j;
+            aP = mx(c0, c1);
+            aM = mx(c2, c3);
+        });
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            t1 = min(t1, __shfl_xor(t1, off));
+            lastbad = max(lastbad, __shfl_xor(lastbad, off));
+        }
+        if (t1 > jend) t1 = jend;
+        int t2 = max(lastbad + 1, j0);
+        if (!okA) t1 = j0;
+        if (!okB) t2 = jend;
+        if (t2 < t1) t2 = t1;
+        const bool split = !(t1 == j0 && t2 == jend);
+        bool exact = split;
+        C64 pre = c64_id(), post = c64_id();
+        if (split) {
+            const int ia = max(0, min(nb - 1, e - vc.emin)) * 16;
+            const int ib = max(0, min(nb - 1, e + 1 - vc.emin)) * 16;
+            walk_piece(pk, k, gi, j0, jend, [&](uint32_t d, int j) {
+                if (j < t1) {
+                    const double2 a = sA[ia + d], b = sB[ia + d];
+                    c64_step(pre, a.x, a.y, b.x, b.y);
+                } else if (j >= t2) {
+                    const double2 a = sA[ib + d], b = sB[ib + d];
+                    c64_step(post, a.x, a.y, b.x, b.y);
+                }
+            });
+            // ordered products over the group (exact: same binade grid throughout)
+#pragma unroll
+            for (int off = 1; off < 16; off <<= 1) {
+                const C64 o1 = shfl_c64(pre, gsrc + ((gi - off) & 15));
+                const C64 o2 = shfl_c64(post, gsrc + ((gi - off) & 15));
+                if (gi >= off) {
+                    pre = c64_mul(o1, pre);
+                    post = c64_mul(o2, post);
+                }
+            }
+            pre = shfl_c64(pre, gsrc + 15);
+            post = shfl_c64(post, gsrc + 15);
+            exact = c64_exact(pre, e, vc.spread) && c64_exact(post, e + 1, vc.spread);
+        }
+        if (gi == 0) {
+            if (exact) {
+                plan[gid] = VitPlan{PLAN_SPLIT, (int8_t)e, (int8_t)(e + 1), 0, (uint16_t)t1,
+                                    (uint16_t)t2};
+                comp3[gid * 2] = make_double4(pre.pp, pre.pm, pre.mp, pre.mm);
+                comp3[gid * 2 + 1] = make_double4(post.pp, post.pm, post.mp, post.mm);
+            } else {
+                plan[gid] = VitPlan{PLAN_SEQ, 0, 0, 0, 0, 0};
+            }
+        }
     }
 }
 
@@ -389,42 +492,52 @@ __device__ __forceinline__ void st_c64(double4* p, const C64& c) {
     *p = make_double4(c.pp, c.pm, c.mp, c.mm);
 }
 
-// sequential reference steps over positions [k*256 + ja, k*256 + jb) of the chunk
-__device__ double2 seq_steps(const uint32_t* __restrict__ pk, const double4* L, int64_t k,
-                             int ja, int jb, double2 v) {
-    if (jb <= ja) return v;
-    int64_t pos = k * kSB + ja;
-    uint32_t w = pk[pos >> 4];
-    uint32_t prevb = base_at(pk, pos - 1);
-    double P = v.x, M = v.y;
-    for (int j = ja; j < jb; ++j, ++pos) {
-        if ((pos & 15) == 0) w = pk[pos >> 4];
-        const uint32_t b = (w >> ((pos & 15) * 2)) & 3u;
-        const uint32_t d = prevb | (b << 2);
-        const double4 l = L[d];
-        const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
-        P = s.P;
-        M = s.M;
-        prevb = b;
+// The serial chain: wave 0 stages the constants of a window's steps in LDS (lanes in
+// parallel), then lane 0 runs the reference recurrence over them; the LDS reads do not
+// depend on the chain, so they issue ahead of it.
+constexpr int kChainT = 1024;
+__device__ __forceinline__ double2 chain_window(const uint32_t* __restrict__ pk,
+                                                const double4* sL, double4* stepL, int64_t k,
+                                                int ja, int jb, double2 v, int lane) {
+    const int n = jb - ja;
+    if (n <= 0) return v;
+    for (int j = lane; j < n; j += 64) {
+        const int64_t pos = k * kSB + ja + j;
+        const uint32_t d = base_at(pk, pos - 1) | (base_at(pk, pos) << 2);
+        stepL[j] = sL[d];
     }
-    return make_double2(P, M);
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    double P = v.x, M = v.y;
+    if (lane == 0) {
+#pragma unroll 8
+        for (int j = 0; j < n; ++j) {
+            const double4 l = stepL[j];
+            const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
+            P = s.P;
+            M = s.M;
+        }
+    }
+    __builtin_amdgcn_wave_barrier();
+    return make_double2(__shfl(P, 0), __shfl(M, 0));
 }
 
-__global__ __launch_bounds__(kThreads) void k_vit_chain(
+__global__ __launch_bounds__(kChainT) void k_vit_chain(
     VitConsts vc, const uint32_t* packed, Geo g, const VitPlan* __restrict__ plan,
     const double4* __restrict__ comp3, const uint8_t* __restrict__ degen,
     double2* __restrict__ entry, double4* __restrict__ gk, double4* __restrict__ gap,
     int32_t* __restrict__ barlist, double2* __restrict__ vout) {
     const int64_t c = blockIdx.x;
     const int t = threadIdx.x;
-    const int64_t per = (g.nsb + kThreads - 1) / kThreads;
-    const int64_t b0 = t * per, b1 = min(b0 + per, g.nsb);
+    const int64_t per = (g.nsb + kChainT - 1) / kChainT;
+    const int64_t b0 = min((int64_t)t * per, g.nsb), b1 = min(b0 + per, g.nsb);
     double2* ent = entry + c * (g.nsb + 1);
     __shared__ double4 sL[16];
+    __shared__ double4 stepL[kSB];
     if (t < 16) sL[t] = make_double4(vc.L[t][0], vc.L[t][1], vc.L[t][2], vc.L[t][3]);
     if (degen[c]) {
         for (int64_t k = b0; k < b1; ++k) ent[k] = make_double2(-DBL_MAX, -DBL_MAX);
-        if (t == kThreads - 1) ent[g.nsb] = make_double2(-DBL_MAX, -DBL_MAX);
+        if (t == kChainT - 1) ent[g.nsb] = make_double2(-DBL_MAX, -DBL_MAX);
         return;
     }
     const uint32_t* pk = chunk_ptr(packed, g, c);
@@ -454,14 +567,14 @@ __global__ __launch_bounds__(kThreads) void k_vit_chain(
     }
     if (!hasb) lead = run;
     // phase 2: segmented scan of (hasb, trail) + barrier count scan
-    __shared__ C64 sM[kThreads];
-    __shared__ int sF[kThreads];
-    __shared__ int sN[kThreads];
+    __shared__ C64 sM[kChainT];
+    __shared__ int sF[kChainT];
+    __shared__ int sN[kChainT];
     sM[t] = run;
     sF[t] = hasb;
     sN[t] = nb;
     __syncthreads();
-    for (int off = 1; off < kThreads; off <<= 1) {
+    for (int off = 1; off < kChainT; off <<= 1) {
         C64 m = sM[t];
         int fl = sF[t], n = sN[t];
         if (t >= off) {
@@ -477,8 +590,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_chain(
     }
     const C64 incoming = t > 0 ? sM[t - 1] : c64_id();
     const int bidx0 = t > 0 ? sN[t - 1] : 0;
-    const int nbar = sN[kThreads - 1];
-    // barrier list in chunk order
+    const int nbar = sN[kChainT - 1];
     {
         int idx = bidx0;
         bool first = true;
@@ -494,10 +606,10 @@ __global__ __launch_bounds__(kThreads) void k_vit_chain(
         }
     }
     __syncthreads();
-    // phase 3: the serial chain over barriers (one lane)
+    // phase 3: the serial chain over barriers (wave 0; lane 0 runs the recurrence)
     const uint32_t o0 = base_at(pk, 0);
     const double2 init = make_double2(vc.logpi[o0], vc.logpi[o0 + 4]);
-    if (t == 0) {
+    if (t < 64) {
         double2 v = init;
         for (int i = 0; i < nbar; ++i) {
             const int64_t k = blc[i];
@@ -505,8 +617,8 @@ __global__ __launch_bounds__(kThreads) void k_vit_chain(
             v = c64_apply(v, ld_c64(gpc + i));
             const int ja = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
             const int jb = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
-            v = seq_steps(pk, sL, k, ja, jb, v);
-            voc[i] = v;
+            v = chain_window(pk, sL, stepL, k, ja, jb, v, t);
+            if (t == 0) voc[i] = v;
         }
     }
     __syncthreads();
@@ -534,10 +646,11 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
                                                           uint4* __restrict__ bp,
                                                           uint8_t* __restrict__ origin,
                                                           uint32_t* status) {
-    __shared__ double4 L[16];
-    if (threadIdx.x < 16)
-        L[threadIdx.x] = make_double4(vc.L[threadIdx.x][0], vc.L[threadIdx.x][1],
-                                      vc.L[threadIdx.x][2], vc.L[threadIdx.x][3]);
+    __shared__ double2 LA[16], LB[16];   // conflict-free halves (256 B each)
+    if (threadIdx.x < 16) {
+        LA[threadIdx.x] = make_double2(vc.L[threadIdx.x][0], vc.L[threadIdx.x][1]);
+        LB[threadIdx.x] = make_double2(vc.L[threadIdx.x][2], vc.L[threadIdx.x][3]);
+    }
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;
@@ -560,8 +673,8 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
         wP0 = wP1 = wM0 = wM1 = 0;
     };
     auto step = [&](uint32_t d, int q, int jj) {
-        const double4 l = L[d];
-        const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
+        const double2 la = LA[d], lb = LB[d];
+        const Step s = ref_step(P, M, la.x, la.y, lb.x, lb.y);
         P = s.P;
         M = s.M;
         const uint32_t noP = s.bP ? oM : oP;
@@ -688,6 +801,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
 // ---------------------------------------------------------------- workspace layout
 struct VitWs {
     int4* comp1;
+    longlong2* aent;
     VitPlan* plan;
     double4* comp3;
     double2* entry;
@@ -716,6 +830,7 @@ VitWs carve(void* base, int64_t nchunks, int64_t nsb) {
     };
     VitWs w;
     w.comp1 = (int4*)take(nt * sizeof(int4));
+    w.aent = (longlong2*)take(nchunks * (nsb + 1) * sizeof(longlong2));
     w.plan = (VitPlan*)take(nt * sizeof(VitPlan));
     w.comp3 = (double4*)take(nt * 2 * sizeof(double4));
     w.entry = (double2*)take(nchunks * (nsb + 1) * sizeof(double2));
@@ -753,13 +868,17 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     const unsigned grid = (unsigned)((nt + kThreads - 1) / kThreads);
     const size_t lds3 = (size_t)(vc.emax - vc.emin + 1) * 16 * sizeof(double4);
     hipLaunchKernelGGL(k_vit_approx, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.comp1);
-    hipLaunchKernelGGL(k_vit_plan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, vc, packed, g,
-                       w.comp1, w.plan, w.degen, w.splitlist, w.splitcount);
+    hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks), dim3(kScanT), 0, s, vc, packed, g,
+                       w.comp1, w.aent, w.degen);
+    hipError_t me = hipMemsetAsync(w.splitcount, 0, nchunks * sizeof(int32_t), s);
+    if (me != hipSuccess) return me;
+    hipLaunchKernelGGL(k_vit_classify, dim3(grid), dim3(kThreads), 0, s, vc, g, w.aent, w.degen,
+                       w.plan, w.splitlist, w.splitcount);
     hipLaunchKernelGGL(k_vit_exact, dim3(grid), dim3(kThreads), lds3, s, vc, d_vt, packed, g,
                        w.plan, w.comp3, status);
-    hipLaunchKernelGGL(k_vit_exact_split, dim3((unsigned)nchunks), dim3(64), 0, s, vc, d_vt,
-                       packed, g, w.plan, w.splitlist, w.splitcount, w.comp3);
-    hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kThreads), 0, s, vc, packed, g,
+    hipLaunchKernelGGL(k_vit_irregular, dim3((unsigned)nchunks), dim3(256), lds3, s, vc, d_vt,
+                       packed, g, w.aent, w.plan, w.splitlist, w.splitcount, w.comp3);
+    hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kChainT), 0, s, vc, packed, g,
                        w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout);
     hipLaunchKernelGGL(k_vit_forward, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.degen,
                        w.entry, w.bp, w.origin, status);
