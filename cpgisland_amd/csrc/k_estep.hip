@@ -71,20 +71,28 @@ __device__ __forceinline__ double rcp_nr(double z) {
     return fma(r, e, r);
 }
 
-// posterior in [0,1] -> unsigned fixed point 2^-47 (round to nearest): a chunk's 65,536
-// positions sum below 2^63, integer LDS atomics are exact and order-independent
+// posterior in [0,1] -> unsigned fixed point 2^-47, rounded to nearest: adding 1.5*2^52
+// puts round(y) in the low mantissa bits (exact for 0 <= y < 2^51); subtracting the
+// constant's bit pattern leaves the integer.  A chunk's 65,536 positions sum below 2^63,
+// so integer LDS atomics are exact and order-independent.
 constexpr double kFix = 140737488355328.0;        // 2^47
-__device__ __forceinline__ unsigned long long to_fixed(double x) {
-    const double y = rint(x * kFix);                 // exact scaling, then round
-    const double hi = floor(y * 0x1.0p-32);
-    const uint32_t h = (uint32_t)hi;
-    const uint32_t l = (uint32_t)fma(-hi, 4294967296.0, y);
-    return ((unsigned long long)h << 32) | l;
+constexpr double kMagic = 6755399441055744.0;     // 1.5 * 2^52
+__device__ __forceinline__ unsigned long long to_fixed_scaled(double y) {   // y = x * 2^47
+    return (unsigned long long)__double_as_longlong(y + kMagic) -
+           (unsigned long long)__double_as_longlong(kMagic);
 }
 
 // the lane's 64 dinucleotide codes (prev | cur << 2), 8 per word, read once from HBM
 struct Codes {
     uint32_t w[8];
+    uint32_t raw[4], prev;   // the lane's packed words and the word before them
+    // 10-bit index of the 5-base window ending at position 4g+3 (4 matrices 4g..4g+3)
+    __device__ __forceinline__ uint32_t win(int g) const {   // g compile-time
+        const int r = g >> 2, s = g & 3;
+        const uint32_t lo = r == 0 ? prev : raw[r - 1];
+        return s == 0 ? (__builtin_amdgcn_alignbit(raw[r], lo, 30) & 0x3FFu)
+                      : ((raw[r] >> (8 * s - 2)) & 0x3FFu);
+    }
     // the 16 codes of mini-block m (runtime m: a select chain, no register indexing)
     __device__ __forceinline__ uint64_t mb(int m) const {
         const uint32_t lo = m == 0 ? w[0] : m == 1 ? w[2] : m == 2 ? w[4] : w[6];
@@ -100,6 +108,8 @@ __device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int
     const uint32_t ww[4] = {v.x, v.y, v.z, v.w};
     uint32_t prev = t > 0 ? pk[4 * t - 1] : 0u;
     Codes c;
+    c.raw[0] = v.x; c.raw[1] = v.y; c.raw[2] = v.z; c.raw[3] = v.w;
+    c.prev = prev;
 #pragma unroll
     for (int k = 0; k < 8; ++k) c.w[k] = 0u;
 #pragma unroll
@@ -125,7 +135,9 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     // conflict-free constant tables: 16 x 16 B each = one 256-B bank row
     double2* TA = reinterpret_cast<double2*>(smem);          // (M(+,+), M(+,-))
     double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
-    auto* bins = reinterpret_cast<unsigned long long*>(TB + 16);   // [wave][4 replicas][64]
+    double2* TA4 = TB + 16;                                   // 4-step products, row 0
+    double2* TB4 = TA4 + 1024;                                //                  row 1
+    auto* bins = reinterpret_cast<unsigned long long*>(TB4 + 1024);   // [wave][4][64]
     Mat* sm = reinterpret_cast<Mat*>(bins + nw * 4 * 64);     // [nl] (scan; then checkpoints)
     const int t = threadIdx.x;
     const int lane = t & 63;
@@ -137,27 +149,58 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         TB[t] = make_double2(model.a[p + 4][b], model.a[p + 4][b + 4]);
     }
     for (int i = t; i < nw * 4 * 64; i += nl) bins[i] = 0ull;
+    // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4)
+    for (int i = t; i < 1024; i += nl) {
+        int b[5];
+#pragma unroll
+        for (int k = 0; k < 5; ++k) b[k] = (i >> (2 * k)) & 3;
+        double x00 = 1.0, x01 = 0.0, x10 = 0.0, x11 = 1.0;
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+            const int p = b[k], q = b[k + 1];
+            const double m00 = model.a[p][q], m01 = model.a[p][q + 4],
+                         m10 = model.a[p + 4][q], m11 = model.a[p + 4][q + 4];
+            const double n00 = x00 * m00 + x01 * m10, n01 = x00 * m01 + x01 * m11;
+            const double n10 = x10 * m00 + x11 * m10, n11 = x10 * m01 + x11 * m11;
+            x00 = n00; x01 = n01; x10 = n10; x11 = n11;
+        }
+        TA4[i] = make_double2(x00, x01);
+        TB4[i] = make_double2(x10, x11);
+    }
     const Codes cd = lane_codes(pk, t);
     __syncthreads();
 
     constexpr int L = kLanePos;            // 64 positions per lane
     constexpr int kMB = 16, NMB = L / kMB;
     const int p0 = t * L;
-    // 1. lane product of M_p over its positions (position 0 carries no matrix)
+    // 1. lane product of M_p over its positions, four matrices per lookup (position 0
+    //    carries no matrix: lane 0's first group is M_1 M_2 M_3)
     Mat P = mid();
-#pragma unroll 1
-    for (int m = 0; m < NMB; ++m) {
-        const uint64_t cm = cd.mb(m);
 #pragma unroll
-        for (int i = 0; i < kMB; ++i) {
-            if (t == 0 && m == 0 && i == 0) continue;
-            const uint32_t d = code_at(cm, i);
-            const double2 ma = TA[d], mb = TB[d];
-            Mat r{P.a * ma.x + P.b * mb.x, P.a * ma.y + P.b * mb.y, P.c * ma.x + P.d * mb.x,
-                  P.c * ma.y + P.d * mb.y, P.e};
-            P = r;
-            if ((i & 7) == 7) mnorm(P);
+    for (int gq = 0; gq < L / 4; ++gq) {
+        double2 ra, rb;
+        if (t == 0 && gq == 0) {
+            double x00 = 1.0, x01 = 0.0, x10 = 0.0, x11 = 1.0;
+            const uint64_t cm = cd.mb(0);
+#pragma unroll
+            for (int i = 1; i < 4; ++i) {
+                const uint32_t d = code_at(cm, i);
+                const double2 ma = TA[d], mb = TB[d];
+                const double n00 = x00 * ma.x + x01 * mb.x, n01 = x00 * ma.y + x01 * mb.y;
+                const double n10 = x10 * ma.x + x11 * mb.x, n11 = x10 * ma.y + x11 * mb.y;
+                x00 = n00; x01 = n01; x10 = n10; x11 = n11;
+            }
+            ra = make_double2(x00, x01);
+            rb = make_double2(x10, x11);
+        } else {
+            const uint32_t wi = cd.win(gq);
+            ra = TA4[wi];
+            rb = TB4[wi];
         }
+        Mat r{P.a * ra.x + P.b * rb.x, P.a * ra.y + P.b * rb.y, P.c * ra.x + P.d * rb.x,
+              P.c * ra.y + P.d * rb.y, P.e};
+        P = r;
+        if ((gq & 1) == 1) mnorm(P);
     }
     // 2a. inclusive prefix (Hillis-Steele)
     sm[t] = P;
@@ -211,20 +254,19 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     double2* ck = reinterpret_cast<double2*>(sm);
     {
         double xP = bP, xM = bM;
-#pragma unroll 1
+#pragma unroll
         for (int m = NMB - 1; m >= 0; --m) {
             ck[m * nl + t] = make_double2(xP, xM);
             if (m == 0) break;
-            const uint64_t cm = cd.mb(m);
 #pragma unroll
-            for (int i = kMB - 1; i >= 0; --i) {
-                const uint32_t d = code_at(cm, i);
-                const double2 ma = TA[d], mb = TB[d];
-                const double nP = ma.x * xP + ma.y * xM, nM = mb.x * xP + mb.y * xM;
+            for (int gq = 4 * m + 3; gq >= 4 * m; --gq) {   // beta_{4g-1} = T4(g) beta_{4g+3}
+                const uint32_t wi = cd.win(gq);
+                const double2 ra = TA4[wi], rb = TB4[wi];
+                const double nP = ra.x * xP + ra.y * xM, nM = rb.x * xP + rb.y * xM;
                 xP = nP;
                 xM = nM;
-                if ((i & 3) == 0) vnorm(xP, xM);
             }
+            vnorm(xP, xM);
         }
     }
     // 3b. mini-blocks: forward alphas in registers, then backward with xi accumulation
@@ -268,12 +310,12 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             const double2 ma = TA[d], mb = TB[d];
             const double x00 = uP * ma.x * yP, x01 = uP * ma.y * yM, x10 = uM * mb.x * yP,
                          x11 = uM * mb.y * yM;
-            const double rz = rcp_nr((x00 + x01) + (x10 + x11));
+            const double rz = rcp_nr((x00 + x01) + (x10 + x11)) * kFix;   // exact scaling
             unsigned long long* bu = wb + d * 4;
-            atomicAdd(bu + 0, to_fixed(x00 * rz));
-            atomicAdd(bu + 1, to_fixed(x01 * rz));
-            atomicAdd(bu + 2, to_fixed(x10 * rz));
-            atomicAdd(bu + 3, to_fixed(x11 * rz));
+            atomicAdd(bu + 0, to_fixed_scaled(x00 * rz));
+            atomicAdd(bu + 1, to_fixed_scaled(x01 * rz));
+            atomicAdd(bu + 2, to_fixed_scaled(x10 * rz));
+            atomicAdd(bu + 3, to_fixed_scaled(x11 * rz));
             const double nP = ma.x * yP + ma.y * yM, nM = mb.x * yP + mb.y * yM;
             yP = nP;
             yM = nM;
@@ -352,7 +394,7 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
     if (C % 4096 || C > (int64_t)kET * kLanePos) return hipErrorInvalidValue;
     const int lanes = (int)(C / kLanePos);
     double* slab = static_cast<double*>(ws);
-    const size_t lds = 32 * sizeof(double2) + (size_t)(lanes / 64) * 4 * 64 * sizeof(double) +
+    const size_t lds = (32 + 2048) * sizeof(double2) + (size_t)(lanes / 64) * 4 * 64 * sizeof(double) +
                        std::max(lanes * sizeof(Mat), (size_t)lanes * (kLanePos / 16) * 16);
     if (nchunks > 0)
         hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,

@@ -35,6 +35,53 @@ struct WordMasks {
     uint32_t S, start, close, C, G, CG;
 };
 
+// masks of one sign word from registers: S, the previous sign word, its two packed words
+// and the packed word before them (0 at the chunk start)
+__device__ __forceinline__ WordMasks masks_reg(uint32_t S, uint32_t Sprev, uint32_t w0,
+                                               uint32_t w1, uint32_t wprev) {
+    WordMasks m;
+    const uint32_t Sp = (S << 1) | (Sprev >> 31);
+    m.S = S;
+    m.start = S & ~Sp;
+    m.close = ~S & Sp;
+    const uint32_t h0 = w0 >> 1, h1 = w1 >> 1;
+    const uint32_t c = compact16(w0 & ~h0) | (compact16(w1 & ~h1) << 16);
+    const uint32_t g = compact16(h0 & ~w0) | (compact16(h1 & ~w1) << 16);
+    m.C = c;
+    m.G = g;
+    m.CG = g & ((c << 1) | ((wprev >> 30) == 1u));
+    return m;
+}
+
+// the 4 sign words a lane owns (w0..w0+3), all loads vectorised; words >= nw read as 0
+__device__ __forceinline__ void masks4(const uint32_t* __restrict__ pk,
+                                       const uint32_t* __restrict__ sg, int64_t w0, int64_t nw,
+                                       WordMasks (&m)[4]) {
+    uint32_t S[4], P[8], sprev, pprev;
+    if (w0 + 4 <= nw) {
+        const uint4 s4 = *reinterpret_cast<const uint4*>(sg + w0);
+        const uint4 p0 = *reinterpret_cast<const uint4*>(pk + 2 * w0);
+        const uint4 p1 = *reinterpret_cast<const uint4*>(pk + 2 * w0 + 4);
+        S[0] = s4.x; S[1] = s4.y; S[2] = s4.z; S[3] = s4.w;
+        P[0] = p0.x; P[1] = p0.y; P[2] = p0.z; P[3] = p0.w;
+        P[4] = p1.x; P[5] = p1.y; P[6] = p1.z; P[7] = p1.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool in = w0 + i < nw;
+            S[i] = in ? sg[w0 + i] : 0u;
+            P[2 * i] = in ? pk[2 * (w0 + i)] : 0u;
+            P[2 * i + 1] = in ? pk[2 * (w0 + i) + 1] : 0u;
+        }
+    }
+    sprev = w0 > 0 ? sg[w0 - 1] : 0u;
+    pprev = w0 > 0 ? pk[2 * w0 - 1] : 0u;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+        m[i] = masks_reg(S[i], i == 0 ? sprev : S[i - 1], P[2 * i], P[2 * i + 1],
+                         i == 0 ? pprev : P[2 * i - 1]);
+}
+
 // masks of sign word w (positions 32w..32w+31) of a chunk; nw = words in the chunk
 __device__ __forceinline__ WordMasks word_masks(const uint32_t* __restrict__ pk,
                                                 const uint32_t* __restrict__ sg, int64_t w) {
@@ -143,9 +190,11 @@ __global__ __launch_bounds__(kAT) void k_isl_a1(const uint32_t* packed, const ui
     const uint32_t* sg = sign + c * nw;
     Cnt5 s{0, 0, 0, 0, 0};
     const int64_t w0 = (int64_t)tile * kTileW + threadIdx.x * 4;
+    WordMasks m[4];
+    if (w0 < nw) masks4(pk, sg, w0, nw, m);
 #pragma unroll
     for (int i = 0; i < 4; ++i)
-        if (w0 + i < nw) s = cadd(s, cnt_of(word_masks(pk, sg, w0 + i)));
+        if (w0 + i < nw) s = cadd(s, cnt_of(m[i]));
     __shared__ Cnt5 sb[kAT];
     Cnt5 tot;
     block_scan(s, sb, tot);
@@ -178,13 +227,10 @@ __global__ __launch_bounds__(kAT) void k_isl_a3(const uint32_t* packed, const ui
     const int64_t w0 = (int64_t)tile * kTileW + threadIdx.x * 4;
     WordMasks m[4];
     Cnt5 s{0, 0, 0, 0, 0};
+    if (w0 < nw) masks4(pk, sg, w0, nw, m);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        if (w0 + i < nw) {
-            m[i] = word_masks(pk, sg, w0 + i);
-            s = cadd(s, cnt_of(m[i]));
-        }
-    }
+    for (int i = 0; i < 4; ++i)
+        if (w0 + i < nw) s = cadd(s, cnt_of(m[i]));
     __shared__ Cnt5 sb[kAT];
     Cnt5 tot;
     Cnt5 e = cadd(block_scan(s, sb, tot), tiles[blockIdx.x]);

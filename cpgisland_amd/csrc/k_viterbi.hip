@@ -117,12 +117,16 @@ __device__ __forceinline__ void walk_block(const uint32_t* __restrict__ pk, int6
     const int64_t wbase = k * kSBWords;
     const int64_t nwords = (C + 15) >> 4;
     uint32_t prev = (k > 0) ? pk[wbase - 1] : 0u;
+    uint4 cur;
+    if (kFull) cur = *reinterpret_cast<const uint4*>(pk + wbase);   // next quad prefetched below
 #pragma unroll 1
     for (int q = 0; q < 4; ++q) {
         uint32_t w[4];
         if (kFull) {
-            const uint4 v = *reinterpret_cast<const uint4*>(pk + wbase + 4 * q);
-            w[0] = v.x; w[1] = v.y; w[2] = v.z; w[3] = v.w;
+            const uint4 nxt =
+                q < 3 ? *reinterpret_cast<const uint4*>(pk + wbase + 4 * (q + 1)) : cur;
+            w[0] = cur.x; w[1] = cur.y; w[2] = cur.z; w[3] = cur.w;
+            cur = nxt;
         } else {
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
@@ -149,6 +153,23 @@ __device__ __forceinline__ void walk_block(const uint32_t* __restrict__ pk, int6
     }
 }
 
+// the 17 packed words a full block reads (its 16 + the one before), all loads in flight
+struct BlockWords {
+    uint32_t w[16], prev;
+};
+__device__ __forceinline__ BlockWords load_block(const uint32_t* __restrict__ pk, int64_t k) {
+    const int64_t wbase = k * kSBWords;
+    BlockWords b;
+    const uint4* p4 = reinterpret_cast<const uint4*>(pk + wbase);
+    const uint4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
+    b.prev = pk[wbase - 1];
+    b.w[0] = a0.x; b.w[1] = a0.y; b.w[2] = a0.z; b.w[3] = a0.w;
+    b.w[4] = a1.x; b.w[5] = a1.y; b.w[6] = a1.z; b.w[7] = a1.w;
+    b.w[8] = a2.x; b.w[9] = a2.y; b.w[10] = a2.z; b.w[11] = a2.w;
+    b.w[12] = a3.x; b.w[13] = a3.y; b.w[14] = a3.z; b.w[15] = a3.w;
+    return b;
+}
+
 struct Geo {
     int64_t nchunks, C, nsb;
     __device__ __forceinline__ bool full(int64_t k) const { return k > 0 && (k + 1) * kSB <= C; }
@@ -165,17 +186,52 @@ __device__ __forceinline__ const uint32_t* chunk_ptr(const uint32_t* packed, con
 }
 
 // ---------------------------------------------------------------- K1: approx composite
+__device__ __forceinline__ int4 i4_mul(const int4 a, const int4 b) {   // max-plus, int32
+    return make_int4(max(a.x + b.x, a.y + b.z), max(a.x + b.y, a.y + b.w),
+                     max(a.z + b.x, a.w + b.z), max(a.z + b.y, a.w + b.w));
+}
+// single-step matrix of dinucleotide d in the (pp, pm, mp, mm) layout from Q = (+->+,
+// -->+, +->-, -->-)
+__device__ __forceinline__ int4 q_mat(const int4 q) { return make_int4(q.x, q.z, q.y, q.w); }
+
 __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uint32_t* packed,
                                                          Geo g, int4* __restrict__ comp) {
     __shared__ int4 Q[16];
+    __shared__ int4 Q4[1024];   // 4-step products over 5-base windows (exact: integers)
     if (threadIdx.x < 16)
         Q[threadIdx.x] = make_int4(vc.Q[threadIdx.x][0], vc.Q[threadIdx.x][1],
                                    vc.Q[threadIdx.x][2], vc.Q[threadIdx.x][3]);
+    __syncthreads();
+    for (int i = threadIdx.x; i < 1024; i += kThreads) {
+        int4 m = q_mat(Q[(i & 3) | (((i >> 2) & 3) << 2)]);
+#pragma unroll
+        for (int k = 1; k < 4; ++k) {
+            const int p = (i >> (2 * k)) & 3, b = (i >> (2 * k + 2)) & 3;
+            m = i4_mul(m, q_mat(Q[p | (b << 2)]));
+        }
+        Q4[i] = m;
+    }
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     const uint32_t* pk = chunk_ptr(packed, g, c);
+    if (g.full(k)) {
+        int4 acc = make_int4(0, kNeg32, kNeg32, 0);
+        const BlockWords bw = load_block(pk, k);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
+#pragma unroll
+            for (int s = 0; s < 4; ++s) {
+                const uint32_t wi = s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 0x3FFu)
+                                           : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
+                acc = i4_mul(acc, Q4[wi]);
+            }
+        }
+        comp[gid] = acc;
+        return;
+    }
     int32_t a = 0, b = kNeg32, e = kNeg32, f = 0;
     auto step = [&](uint32_t d, int, int) {
         const int4 q = Q[d];
@@ -183,8 +239,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uin
         int32_t ne = max(e + q.x, f + q.y), nf = max(e + q.z, f + q.w);
         a = na; b = nb; e = ne; f = nf;
     };
-    if (g.full(k)) walk_block<true>(pk, k, g.C, step);
-    else walk_block<false>(pk, k, g.C, step);
+    walk_block<false>(pk, k, g.C, step);
     comp[gid] = make_int4(a, b, e, f);
 }
 
@@ -291,15 +346,29 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
                                                         VitPlan* __restrict__ plan,
                                                         double4* __restrict__ comp3,
                                                         uint32_t* status) {
-    // [e - emin][16] x 16 B per half: each half-table of a binade is one 256-B bank row
+    // per binade slot: single-step halves sA/sB [16] (one 256-B bank row each) and 2-step
+    // composites over 3-base windows, halves P2A = (pp, pm), P2B = (mp, mm) [64].  Every
+    // entry is a sum of binade-rounded constants: exact on the binade's grid.
     extern __shared__ __attribute__((aligned(16))) double2 sLe[];
     const int nb = vc.emax - vc.emin + 1;
     double2* sA = sLe;
-    double2* sB = sLe + nb * 16;
+    double2* sB = sA + nb * 16;
+    double2* P2A = sB + nb * 16;
+    double2* P2B = P2A + nb * 64;
     for (int i = threadIdx.x; i < nb * 16; i += kThreads) {
         const double* s = vt->Le[vc.emin + i / 16][i % 16];
         sA[i] = make_double2(s[0], s[1]);
         sB[i] = make_double2(s[2], s[3]);
+    }
+    for (int i = threadIdx.x; i < nb * 64; i += kThreads) {
+        const int e = vc.emin + i / 64, w = i % 64;
+        const double* l1 = vt->Le[e][(w & 3) | (((w >> 2) & 3) << 2)];          // x -> y
+        const double* l2 = vt->Le[e][((w >> 2) & 3) | (((w >> 4) & 3) << 2)];   // y -> z
+        // composite of one step: (pp, pm, mp, mm) = (l0, l2, l1, l3)
+        C64 m{l1[0], l1[2], l1[1], l1[3]};
+        c64_step(m, l2[0], l2[1], l2[2], l2[3]);
+        P2A[i] = make_double2(m.pp, m.pm);
+        P2B[i] = make_double2(m.mp, m.mm);
     }
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -308,15 +377,31 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     if (p.type != PLAN_REGULAR) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     const uint32_t* pk = chunk_ptr(packed, g, c);
-    const double2* ta = sA + (p.e_pre - vc.emin) * 16;
-    const double2* tb = sB + (p.e_pre - vc.emin) * 16;
+    const int slot = p.e_pre - vc.emin;
     C64 acc = c64_id();
-    auto step = [&](uint32_t d, int, int) {
-        const double2 a = ta[d], b = tb[d];
-        c64_step(acc, a.x, a.y, b.x, b.y);
-    };
-    if (g.full(k)) walk_block<true>(pk, k, g.C, step);
-    else walk_block<false>(pk, k, g.C, step);
+    if (g.full(k)) {
+        const double2* pa = P2A + slot * 64;
+        const double2* pb = P2B + slot * 64;
+        const BlockWords bw = load_block(pk, k);
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
+#pragma unroll
+            for (int s = 0; s < 8; ++s) {
+                const uint32_t wi = s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 63u)
+                                           : ((bw.w[r] >> (4 * s - 2)) & 63u);
+                const double2 a = pa[wi], b = pb[wi];
+                acc = c64_mul(acc, C64{a.x, a.y, b.x, b.y});
+            }
+        }
+    } else {
+        const double2* ta = sA + slot * 16;
+        const double2* tb = sB + slot * 16;
+        walk_block<false>(pk, k, g.C, [&](uint32_t d, int, int) {
+            const double2 a = ta[d], b = tb[d];
+            c64_step(acc, a.x, a.y, b.x, b.y);
+        });
+    }
     if (!c64_exact(acc, p.e_pre, vc.spread)) {
         plan[gid].type = PLAN_SEQ;   // exactness not guaranteed: let K4 run it sequentially
         return;
@@ -496,6 +581,8 @@ __device__ __forceinline__ void st_c64(double4* p, const C64& c) {
 // parallel), then lane 0 runs the reference recurrence over them; the LDS reads do not
 // depend on the chain, so they issue ahead of it.
 constexpr int kChainT = 1024;
+constexpr int kMaxStagedBar = 64;     // barriers staged in LDS per chunk
+constexpr int kStageSteps = 1536;     // window steps staged in LDS per chunk
 __device__ __forceinline__ double2 chain_window(const uint32_t* __restrict__ pk,
                                                 const double4* sL, double4* stepL, int64_t k,
                                                 int ja, int jb, double2 v, int lane) {
@@ -534,6 +621,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     double2* ent = entry + c * (g.nsb + 1);
     __shared__ double4 sL[16];
     __shared__ double4 stepL[kSB];
+    __shared__ double4 stageL[kStageSteps];
     if (t < 16) sL[t] = make_double4(vc.L[t][0], vc.L[t][1], vc.L[t][2], vc.L[t][3]);
     if (degen[c]) {
         for (int64_t k = b0; k < b1; ++k) ent[k] = make_double2(-DBL_MAX, -DBL_MAX);
@@ -606,19 +694,81 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         }
     }
     __syncthreads();
-    // phase 3: the serial chain over barriers (wave 0; lane 0 runs the recurrence)
+    // phase 3: the serial chain over barriers.  The whole workgroup first stages every
+    // window's step constants and every gap composite in LDS, so lane 0's serial
+    // recurrence never waits on global memory; windows beyond the staging capacity fall
+    // back to per-window staging by wave 0.
     const uint32_t o0 = base_at(pk, 0);
     const double2 init = make_double2(vc.logpi[o0], vc.logpi[o0 + 4]);
+    __shared__ int sWoff[kMaxStagedBar + 1];
+    __shared__ int sWa[kMaxStagedBar], sWb[kMaxStagedBar];
+    __shared__ int64_t sWk[kMaxStagedBar];
+    __shared__ C64 sGap[kMaxStagedBar];
+    const int nst = min(nbar, kMaxStagedBar);
+    if (t < nst) {
+        const int64_t k = blc[t];
+        const VitPlan p = pl[k];
+        sWk[t] = k;
+        sWa[t] = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
+        sWb[t] = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
+        sGap[t] = ld_c64(gpc + t);
+    }
+    __syncthreads();
+    if (t == 0) {
+        int o = 0;
+        for (int i = 0; i < nst; ++i) {
+            sWoff[i] = o;
+            const int len = max(0, sWb[i] - sWa[i]);
+            o = (o + len <= kStageSteps) ? o + len : kStageSteps + 1;   // overflow marker
+        }
+        sWoff[nst] = o;
+    }
+    __syncthreads();
+    for (int i = t >> 6; i < nst; i += kChainT / 64) {   // one wave per window
+        const int off = sWoff[i];
+        const int len = max(0, sWb[i] - sWa[i]);
+        if (off + len > kStageSteps) continue;
+        for (int j = t & 63; j < len; j += 64) {
+            const int64_t pos = sWk[i] * kSB + sWa[i] + j;
+            const uint32_t d = base_at(pk, pos - 1) | (base_at(pk, pos) << 2);
+            stageL[off + j] = sL[d];
+        }
+    }
+    __syncthreads();
     if (t < 64) {
         double2 v = init;
         for (int i = 0; i < nbar; ++i) {
-            const int64_t k = blc[i];
-            const VitPlan p = pl[k];
-            v = c64_apply(v, ld_c64(gpc + i));
-            const int ja = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
-            const int jb = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
-            v = chain_window(pk, sL, stepL, k, ja, jb, v, t);
-            if (t == 0) voc[i] = v;
+            if (i < nst && sWoff[i] + max(0, sWb[i] - sWa[i]) <= kStageSteps) {
+                const C64 gp = sGap[i];
+                v = c64_apply(v, gp);
+                if (t == 0) {
+                    double P = v.x, M = v.y;
+                    const double4* st = stageL + sWoff[i];
+                    const int len = sWb[i] - sWa[i];
+#pragma unroll 8
+                    for (int j = 0; j < len; ++j) {
+                        const double4 l = st[j];
+                        const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
+                        P = s.P;
+                        M = s.M;
+                    }
+                    v = make_double2(P, M);
+                    voc[i] = v;
+                }
+                v = make_double2(__shfl(v.x, 0), __shfl(v.y, 0));
+            } else {
+                const int64_t k = blc[i];
+                const VitPlan p = pl[k];
+                v = c64_apply(v, ld_c64(gpc + i));
+                const int ja = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
+                const int jb = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
+                v = chain_window(pk, sL, stepL, k, ja, jb, v, t);
+                if (t == 0) voc[i] = v;
+            }
+#ifdef CPG_DEBUG_CHAIN
+            if (t == 0 && c == 0)
+                printf("chain c0 barrier %d of %d staged %d\n", i, nbar, (int)(i < nst));
+#endif
         }
     }
     __syncthreads();
@@ -874,7 +1024,8 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     if (me != hipSuccess) return me;
     hipLaunchKernelGGL(k_vit_classify, dim3(grid), dim3(kThreads), 0, s, vc, g, w.aent, w.degen,
                        w.plan, w.splitlist, w.splitcount);
-    hipLaunchKernelGGL(k_vit_exact, dim3(grid), dim3(kThreads), lds3, s, vc, d_vt, packed, g,
+    const size_t lds3x = (size_t)(vc.emax - vc.emin + 1) * (16 + 64) * 2 * sizeof(double2);
+    hipLaunchKernelGGL(k_vit_exact, dim3(grid), dim3(kThreads), lds3x, s, vc, d_vt, packed, g,
                        w.plan, w.comp3, status);
     hipLaunchKernelGGL(k_vit_irregular, dim3((unsigned)nchunks), dim3(256), lds3, s, vc, d_vt,
                        packed, g, w.aent, w.plan, w.splitlist, w.splitcount, w.comp3);

@@ -3,7 +3,7 @@
 set -e
 cd "$(dirname "$0")/../cpgisland_amd/csrc"
 BASE='-O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function -Wno-unused-variable --offload-arch=gfx950 -munsafe-fp-atomics'
-for v in base:"" plain:"-DCPG_ABL_PLAIN_STORE" fixed:"-DCPG_ESTEP_FIXED"; do
+for v in dbgchain:"-DCPG_DEBUG_CHAIN"; do
   name=${v%%:*}; flags=${v#*:}
   make -s -j8 OBJDIR=../../build/abl/obj_$name OUT=../../build/abl/libcpg_$name.so CXXFLAGS="$BASE $flags"
 done
