@@ -18,7 +18,6 @@ import os
 import sys
 import time
 
-import numpy as np
 import torch
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
@@ -87,6 +86,7 @@ def main():
 
     from cpgisland_amd import Context, HmmModel
     from cpgisland_amd import device as D
+    from cpgisland_amd import dist as cdist
 
     N = args.bases
     start = rank * SHARD_STRIDE if N <= SHARD_STRIDE else rank * ((N + DECODE - 1) // DECODE * DECODE)
@@ -106,18 +106,14 @@ def main():
     icap = 1 << 20
     iout = torch.empty((icap, 32), dtype=torch.uint8, device=dev)
     icnt = torch.zeros(1, dtype=torch.int64, device=dev)
-    gath = torch.empty((world, 105), dtype=torch.float64, device=dev) if dist else None
     flush = torch.empty(args.flush_mb << 18, dtype=torch.float32, device=dev) if args.flush_mb else None
 
     # trained model for the decode: one Baum-Welch iteration from the reference's model
     D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
-    c = ecnt.cpu().numpy()
     if dist:
-        allc = [torch.empty_like(ecnt) for _ in range(world)]
-        torch.distributed.all_gather(allc, ecnt)
-        c = np.sum([x.cpu().numpy() for x in allc], axis=0)
+        cdist.merge_counts_f64(ecnt)
     from cpgisland_amd import baumwelch
-    model1 = baumwelch.normalize(c)
+    model1 = baumwelch.normalize(ecnt.cpu().numpy())
 
     ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
           for k in ("estep", "counts", "reduce", "viterbi", "islands")}
@@ -135,9 +131,8 @@ def main():
         mark("counts", 1)
         mark("reduce", 0)
         if dist:   # the reducer: int64 sums are exact in any order; fp64 in rank order
-            torch.distributed.all_reduce(lcnt)
-            torch.distributed.all_gather_into_tensor(gath, ecnt)
-            ecnt.copy_(gath.sum(dim=0))
+            cdist.merge_counts_i64(lcnt)
+            cdist.merge_counts_f64(ecnt)
         mark("reduce", 1)
         mark("viterbi", 0)
         D.viterbi(ctx, model1, dp, N, DECODE, sign_out=so, score=score)

@@ -7,7 +7,8 @@
   driver   -> run()        iterate until converged or max_iter (convergence rule:
                            Mahout HmmTrainer's — the MAHOUT-627 rule is unpinned)
 Multi-GPU: each rank runs the mapper on its shard; the stripes are all-gathered and summed
-in rank order (deterministic), then every rank normalises identically (no broadcast).
+in rank order (dist.merge_counts_f64: deterministic), then every rank normalises identically
+(no broadcast).
 """
 from __future__ import annotations
 
@@ -15,7 +16,7 @@ import math
 
 import numpy as np
 
-from . import _lib
+from . import _lib, dist
 from ._lib import check, lib, ptr
 from .hmm import Context, HmmModel
 
@@ -45,30 +46,40 @@ def converged(old: HmmModel, new: HmmModel, epsilon: float) -> bool:
 
 
 def estep(ctx: Context, model: HmmModel, packed, nbases: int,
-          chunk_len: int = _lib.TRAIN_CHUNK, allgather=None):
+          chunk_len: int = _lib.TRAIN_CHUNK, group=None, distributed: bool = False):
     """The mapper over one shard (device tensor) -> host counts (105 doubles).  With
-    `allgather` (torch.distributed), stripes of all ranks are summed in rank order."""
-    import torch
+    `distributed`, the stripes of all ranks are summed in rank order (dist.merge_counts_f64):
+    every rank gets the same bits."""
     from . import device as D
     out = D.bw_estep(ctx, model, packed, nbases, chunk_len)
-    if allgather is not None:
-        ws = allgather.get_world_size()
-        buf = torch.empty((ws, out.numel()), dtype=out.dtype, device=out.device)
-        allgather.all_gather_into_tensor(buf, out)
-        return buf.cpu().numpy().sum(axis=0)
+    if distributed:
+        dist.merge_counts_f64(out, group)
     return out.cpu().numpy()
 
 
-def run(ctx: Context, packed, nbases: int, model: HmmModel | None = None,
+def run(ctx: Context | None, packed, nbases: int, model: HmmModel | None = None,
         convergence: float = 0.005, max_iter: int = 10,
-        chunk_len: int = _lib.TRAIN_CHUNK, allgather=None):
+        chunk_len: int = _lib.TRAIN_CHUNK, distributed: bool = False, group=None,
+        mapper=None):
     """runBaumWelchMR(conf, input, modelIn, output, ..., convergence, "rescaling", numIter).
+    `mapper(model) -> torch tensor of 105 doubles` overrides the shard's E-step (default:
+    the GPU kernel over `packed`); the reducer merge and the loop are the same either way.
     Returns (trained model, iterations run, log-likelihood of the last E-step)."""
+    import torch
+    from . import device as D
+    if mapper is None:
+        def mapper(m):
+            return D.bw_estep(ctx, m, packed, nbases, chunk_len)
     model = model or HmmModel.initial()
     ll = -math.inf
     it = 0
     for it in range(1, max_iter + 1):
-        counts = estep(ctx, model, packed, nbases, chunk_len, allgather)
+        t = mapper(model)
+        if not isinstance(t, torch.Tensor):
+            t = torch.as_tensor(np.asarray(t, dtype=np.float64))
+        if distributed:
+            dist.merge_counts_f64(t, group)
+        counts = t.cpu().numpy()
         ll = float(counts[-1])
         new = normalize(counts)
         done = converged(model, new, convergence)

@@ -31,6 +31,16 @@ namespace {
 constexpr int kET = 1024;               // max lanes per chunk
 constexpr int kLanePos = 64;            // positions per lane
 constexpr int kSlab = 73;               // trans[64] (by dinucleotide x 4) | init[8] | loglik
+// xi bins of one 16-lane replica: [k = from,to pair][d] (64 x u64) padded to 80 so that the
+// two replicas an LDS pass serves sit in opposite bank halves (80 * 8 B = 640 B = 160 banks)
+#ifndef EST_REP
+#define EST_REP 80
+#endif
+#ifndef EST_KD
+#define EST_KD 1
+#endif
+constexpr int kRep = EST_REP;
+__device__ __forceinline__ int bin_of(int d, int k) { return EST_KD ? k * 16 + d : d * 4 + k; }
 
 struct Mat {
     double a, b, c, d;   // [[a b] [c d]]
@@ -137,8 +147,8 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
     double2* TA4 = TB + 16;                                   // 4-step products, row 0
     double2* TB4 = TA4 + 1024;                                //                  row 1
-    auto* bins = reinterpret_cast<unsigned long long*>(TB4 + 1024);   // [wave][4][64]
-    Mat* sm = reinterpret_cast<Mat*>(bins + nw * 4 * 64);     // [nl] (scan; then checkpoints)
+    auto* bins = reinterpret_cast<unsigned long long*>(TB4 + 1024);   // [wave][4][kRep]
+    Mat* sm = reinterpret_cast<Mat*>(bins + nw * 4 * kRep);   // [nl] (scan; then checkpoints)
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int64_t c = blockIdx.x;
@@ -148,7 +158,7 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         TA[t] = make_double2(model.a[p][b], model.a[p][b + 4]);
         TB[t] = make_double2(model.a[p + 4][b], model.a[p + 4][b + 4]);
     }
-    for (int i = t; i < nw * 4 * 64; i += nl) bins[i] = 0ull;
+    for (int i = t; i < nw * 4 * kRep; i += nl) bins[i] = 0ull;
     // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4)
     for (int i = t; i < 1024; i += nl) {
         int b[5];
@@ -270,7 +280,7 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         }
     }
     // 3b. mini-blocks: forward alphas in registers, then backward with xi accumulation
-    unsigned long long* wb = bins + ((t >> 6) * 4 + (lane >> 4)) * 64;   // 16-lane replica
+    unsigned long long* wb = bins + ((t >> 6) * 4 + (lane >> 4)) * kRep;   // 16-lane replica
     double g0P = 0.0, g0M = 0.0;
     double bfP = aP, bfM = aM;   // alpha at the position before the mini-block
 #pragma unroll 1
@@ -311,11 +321,10 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             const double x00 = uP * ma.x * yP, x01 = uP * ma.y * yM, x10 = uM * mb.x * yP,
                          x11 = uM * mb.y * yM;
             const double rz = rcp_nr((x00 + x01) + (x10 + x11)) * kFix;   // exact scaling
-            unsigned long long* bu = wb + d * 4;
-            atomicAdd(bu + 0, to_fixed_scaled(x00 * rz));
-            atomicAdd(bu + 1, to_fixed_scaled(x01 * rz));
-            atomicAdd(bu + 2, to_fixed_scaled(x10 * rz));
-            atomicAdd(bu + 3, to_fixed_scaled(x11 * rz));
+            atomicAdd(wb + bin_of(d, 0), to_fixed_scaled(x00 * rz));
+            atomicAdd(wb + bin_of(d, 1), to_fixed_scaled(x01 * rz));
+            atomicAdd(wb + bin_of(d, 2), to_fixed_scaled(x10 * rz));
+            atomicAdd(wb + bin_of(d, 3), to_fixed_scaled(x11 * rz));
             const double nP = ma.x * yP + ma.y * yM, nM = mb.x * yP + mb.y * yM;
             yP = nP;
             yM = nM;
@@ -327,9 +336,10 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     __syncthreads();
     // slab is counter-major: [kSlab][nchunks]
     const int64_t nch = gridDim.x;
-    if (t < 64) {
+    if (t < 64) {   // slab row t = d * 4 + k
         unsigned long long s = 0;
-        for (int r = 0; r < nw * 4; ++r) s += bins[r * 64 + t];
+        const int b = bin_of(t >> 2, t & 3);
+        for (int r = 0; r < nw * 4; ++r) s += bins[r * kRep + b];
         slab[t * nch + c] = (double)s * (1.0 / kFix);
     }
     if (t == 0) {
@@ -394,7 +404,7 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
     if (C % 4096 || C > (int64_t)kET * kLanePos) return hipErrorInvalidValue;
     const int lanes = (int)(C / kLanePos);
     double* slab = static_cast<double*>(ws);
-    const size_t lds = (32 + 2048) * sizeof(double2) + (size_t)(lanes / 64) * 4 * 64 * sizeof(double) +
+    const size_t lds = (32 + 2048) * sizeof(double2) + (size_t)(lanes / 64) * 4 * kRep * sizeof(double) +
                        std::max(lanes * sizeof(Mat), (size_t)lanes * (kLanePos / 16) * 16);
     if (nchunks > 0)
         hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,

@@ -99,8 +99,11 @@ __device__ __forceinline__ Step ref_step(double P, double M, double l0, double l
     Step s;
     s.bP = cmp > cpp;
     s.bM = cmm > cpm;
-    s.P = s.bP ? cmp : cpp;
-    s.M = s.bM ? cmm : cpm;
+    // the survivor value is the max either way: on a tie both candidates are the same
+    // double (sums of finite values or -inf never give NaN or -0), so v_max_f64 replaces
+    // two 32-bit selects per state
+    s.P = fmax(cpp, cmp);
+    s.M = fmax(cpm, cmm);
     return s;
 }
 
@@ -170,6 +173,31 @@ __device__ __forceinline__ BlockWords load_block(const uint32_t* __restrict__ pk
     return b;
 }
 
+// dinucleotide code of step j (compile-time) of a full block; j = 0 pairs with the word before
+__device__ __forceinline__ uint32_t bw_code(const BlockWords& b, int j) {
+    const int r = j >> 4, i = j & 15;
+    const uint32_t lo = r == 0 ? b.prev : b.w[r - 1];
+    return i == 0 ? (__builtin_amdgcn_alignbit(b.w[r], lo, 30) & 15u)
+                  : ((b.w[r] >> (2 * i - 2)) & 15u);
+}
+
+// Software-pipelined table walk over NSTEP compile-time steps: the LDS lookup of step j + G
+// is issued before step j is consumed, so G lookups are in flight behind the dependent
+// recurrence (the blocks' lanes are few per SIMD: latency, not bandwidth, is the limit).
+template <int G, int NSTEP, class Idx, class Fetch, class Use>
+__device__ __forceinline__ void pipelined(Idx&& idx, Fetch&& fetch, Use&& use) {
+    using V = decltype(fetch(0u));
+    V ring[G];
+#pragma unroll
+    for (int j = 0; j < G; ++j) ring[j] = fetch(idx(j));
+#pragma unroll
+    for (int j = 0; j < NSTEP; ++j) {
+        const V v = ring[j % G];
+        if (j + G < NSTEP) ring[j % G] = fetch(idx(j + G));
+        use(v, j);
+    }
+}
+
 struct Geo {
     int64_t nchunks, C, nsb;
     __device__ __forceinline__ bool full(int64_t k) const { return k > 0 && (k + 1) * kSB <= C; }
@@ -219,16 +247,14 @@ __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uin
     if (g.full(k)) {
         int4 acc = make_int4(0, kNeg32, kNeg32, 0);
         const BlockWords bw = load_block(pk, k);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
-#pragma unroll
-            for (int s = 0; s < 4; ++s) {
-                const uint32_t wi = s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 0x3FFu)
-                                           : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
-                acc = i4_mul(acc, Q4[wi]);
-            }
-        }
+        pipelined<4, 64>(
+            [&](int j) {   // 5-base window of steps 4j .. 4j+3
+                const int r = j >> 2, s = j & 3;
+                const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
+                return s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 0x3FFu)
+                              : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
+            },
+            [&](uint32_t wi) { return Q4[wi]; }, [&](const int4 q, int) { acc = i4_mul(acc, q); });
         comp[gid] = acc;
         return;
     }
@@ -383,17 +409,15 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
         const double2* pa = P2A + slot * 64;
         const double2* pb = P2B + slot * 64;
         const BlockWords bw = load_block(pk, k);
-#pragma unroll
-        for (int r = 0; r < 16; ++r) {
-            const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
-#pragma unroll
-            for (int s = 0; s < 8; ++s) {
-                const uint32_t wi = s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 63u)
-                                           : ((bw.w[r] >> (4 * s - 2)) & 63u);
-                const double2 a = pa[wi], b = pb[wi];
-                acc = c64_mul(acc, C64{a.x, a.y, b.x, b.y});
-            }
-        }
+        pipelined<4, 128>(
+            [&](int j) {   // 3-base window of steps 2j, 2j+1
+                const int r = j >> 3, s = j & 7;
+                const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
+                return s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 63u)
+                              : ((bw.w[r] >> (4 * s - 2)) & 63u);
+            },
+            [&](uint32_t wi) { return C64{pa[wi].x, pa[wi].y, pb[wi].x, pb[wi].y}; },
+            [&](const C64& m, int) { acc = c64_mul(acc, m); });
     } else {
         const double2* ta = sA + slot * 16;
         const double2* tb = sB + slot * 16;
@@ -822,9 +846,8 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
         o[2 * q] = wP0; o[2 * q + 1] = wP1; o[8 + 2 * q] = wM0; o[8 + 2 * q + 1] = wM1;
         wP0 = wP1 = wM0 = wM1 = 0;
     };
-    auto step = [&](uint32_t d, int q, int jj) {
-        const double2 la = LA[d], lb = LB[d];
-        const Step s = ref_step(P, M, la.x, la.y, lb.x, lb.y);
+    auto step2 = [&](double l0, double l1, double l2, double l3, int q, int jj) {
+        const Step s = ref_step(P, M, l0, l1, l2, l3);
         P = s.P;
         M = s.M;
         const uint32_t noP = s.bP ? oM : oP;
@@ -835,8 +858,40 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
         else { wP1 |= s.bP << (jj - 32); wM1 |= s.bM << (jj - 32); }
         if (jj == 63) flush(q);
     };
+    auto step = [&](uint32_t d, int q, int jj) {
+        const double2 la = LA[d], lb = LB[d];
+        step2(la.x, la.y, lb.x, lb.y, q, jj);
+    };
     if (g.full(k)) {
-        walk_block<true>(pk, k, g.C, step);
+        // quads of 64 steps; the ring of kLook lookups in flight runs across quad borders
+        constexpr int kLook = 4;
+        auto fetch = [&](uint32_t d) { return C64{LA[d].x, LA[d].y, LB[d].x, LB[d].y}; };
+        auto code = [](const uint4 w, uint32_t prev, int j) {   // j compile-time, < 64
+            const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+            const int r = j >> 4, i = j & 15;
+            const uint32_t lo = r == 0 ? prev : ww[r - 1];
+            return i == 0 ? (__builtin_amdgcn_alignbit(ww[r], lo, 30) & 15u)
+                          : ((ww[r] >> (2 * i - 2)) & 15u);
+        };
+        const int64_t wbase = k * kSBWords;
+        uint32_t prev = pk[wbase - 1];
+        uint4 cur = *reinterpret_cast<const uint4*>(pk + wbase);
+        C64 ring[kLook];
+#pragma unroll
+        for (int j = 0; j < kLook; ++j) ring[j] = fetch(code(cur, prev, j));
+#pragma unroll 1
+        for (int q = 0; q < 4; ++q) {
+            const uint4 nxt = *reinterpret_cast<const uint4*>(pk + wbase + 4 * (q < 3 ? q + 1 : q));
+#pragma unroll
+            for (int jj = 0; jj < 64; ++jj) {
+                const C64 l = ring[jj % kLook];
+                const int j2 = jj + kLook;   // past the block's end (q == 3): harmless lookups
+                ring[jj % kLook] = fetch(j2 < 64 ? code(cur, prev, j2) : code(nxt, cur.w, j2 - 64));
+                step2(l.pp, l.pm, l.mp, l.mm, q, jj);
+            }
+            prev = cur.w;
+            cur = nxt;
+        }
     } else {
         // partial/first block: positions outside the chunk are skipped; flush every quad
         walk_block<false>(pk, k, g.C, [&](uint32_t d, int q, int jj) {
@@ -915,25 +970,35 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
         wM[0] = x2.x; wM[1] = x2.y; wM[2] = x2.z; wM[3] = x2.w;
         wM[4] = x3.x; wM[5] = x3.y; wM[6] = x3.z; wM[7] = x3.w;
     }
-    const int j0 = g.jfirst(k), jend = g.jend(k);
-    uint32_t s = endst[gid];
+    // Word-parallel traceback.  Position j's backpointers are a map m_j: state at j ->
+    // state at j-1 (m_j(+) = ~bP_j, m_j(-) = ~bM_j; identity past the block's end).  The
+    // states of a word's 32 positions are H_j(s_31) with H_j = m_{j+1} o ... o m_31: a
+    // 5-level suffix scan of map compositions on bit vectors (X = map(+), Y = map(-) per
+    // bit; f o g = (bfi(Xg, Xf, Yf), bfi(Yg, Xf, Yf))), then m_0 steps into the next word.
+    const int jend = g.jend(k);
+    uint32_t s = endst[gid];   // state at the block's last position
     uint32_t out[8];
 #pragma unroll
     for (int w = 7; w >= 0; --w) {
-        uint32_t o = 0;
+        const int n = jend - 32 * w;
+        const uint32_t vm = n >= 32 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (1u << n) - 1u);
+        const uint32_t A = ~wP[w] | ~vm, B = ~wM[w] & vm;
+        uint32_t X = (A >> 1) | 0x80000000u, Y = B >> 1;   // e_j = m_{j+1}, e_31 = id
 #pragma unroll
-        for (int i = 31; i >= 0; --i) {
-            const int j = w * 32 + i;
-            if (j >= j0 && j < jend) {
-                o |= s << i;
-                const uint32_t bit = ((s ? wP[w] : wM[w]) >> i) & 1u;
-                s = bit ^ 1u;
-            }
+        for (int d = 1; d < 32; d <<= 1) {
+            const uint32_t Xg = __builtin_amdgcn_alignbit(0xFFFFFFFFu, X, d);   // id fill
+            const uint32_t Yg = Y >> d;
+            const uint32_t nX = (Xg & X) | (~Xg & Y), nY = (Yg & X) | (~Yg & Y);
+            X = nX;
+            Y = nY;
         }
-        out[w] = o;
+        const uint32_t S = s ? X : Y;
+        out[w] = S & vm;
+        s = (S & 1u) ? (A & 1u) : (B & 1u);   // state at position 32w - 1
     }
-    if (k == 0) out[0] |= s;   // position 0
-    else if (s != endst[gid - 1]) atomicOr(status, ST_VERIFY_CHAIN);
+    // block 0: bit 0 of out[0] is the state of position 0 itself; otherwise the state
+    // reached before the block must be the previous block's end state
+    if (k > 0 && s != endst[gid - 1]) atomicOr(status, ST_VERIFY_CHAIN);
     // write the block's words (positions k*256 ... k*256+255 of the chunk)
     uint32_t* so = sign_out + c * (g.C >> 5) + k * 8;
     const int64_t nw = (g.C + 31) >> 5;

@@ -1,0 +1,128 @@
+"""Multi-process (world size 2 and 3, gloo on CPU) tests of the multi-GPU host layer
+(cpgisland_amd/dist.py, baumwelch.run(distributed=True)).
+
+The per-shard compute is the oracle here (test infrastructure, CPU), standing in for the
+per-rank GPU kernels, so that the sharding, the reducer merges and the island gather — the
+code that runs unchanged over RCCL on the GPU box — are checked against the unsharded run.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from cpgisland_amd import HmmModel
+from cpgisland_amd import dist as cd
+from cpgisland_amd import _lib
+from oracle import coracle as co
+from oracle import pyref as pr
+
+TRAIN = 4096          # small chunks keep the oracle fast; the logic is size-independent
+DECODE = 65536
+N = 5 * DECODE + 1234  # 5 whole decode chunks + a tail both stages drop
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _genome():
+    from cpgisland_amd import device as D
+    packed, sign = D.synth_host(4242, 0, N)
+    return pr.unpack(packed, N), pr.unpack_bits(sign, N)
+
+
+def _worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        obs, truth = _genome()
+        start, n = cd.shard_bounds(N, world, rank, align=DECODE)
+        o, tr = obs[start:start + n], truth[start:start + n]
+        m = co.initial_model()
+        # labelled counts: int64 all-reduce
+        li = cd.merge_counts_i64(torch.from_numpy(co.count_labelled(o, tr, TRAIN)))
+        # E-step counts: all-gather + rank-order sum (identical bits on every rank)
+        part = co.estep(m, o, TRAIN)
+        fe = cd.merge_counts_f64(torch.from_numpy(part.copy()))
+        # decode: per shard, global chunk numbering, gathered in genome order
+        recs = [co.islands(co.viterbi8(m, o[c * DECODE:(c + 1) * DECODE])[0],
+                           start // DECODE + c) for c in range(n // DECODE)]
+        isl = np.concatenate(recs) if recs else np.zeros(0, co.ISLAND_DTYPE)
+        gi = cd.gather_islands(isl.view(_lib.ISLAND_DTYPE), torch.device("cpu"))
+        # Baum-Welch driver over the shards (oracle mapper), 3 iterations
+        bw, it, ll = __import__("cpgisland_amd.baumwelch", fromlist=["run"]).run(
+            None, None, n, max_iter=3, convergence=0.0, distributed=True,
+            mapper=lambda mm: torch.from_numpy(co.estep(mm.to_struct(), o, TRAIN)))
+        q.put((rank, start, n, li.numpy(), fe.numpy(), part, gi.view(np.uint8).copy(),
+               bw.to_struct(), it, ll))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_sharded_pass_equals_unsharded(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_worker, args=(world, _free_port(), q), nprocs=world, join=True,
+                       start_method="spawn")
+    res = sorted([q.get() for _ in range(world)], key=lambda r: r[0])
+    obs, truth = _genome()
+    m = co.initial_model()
+    # shards tile the genome, whole decode chunks each, the tail on the last rank
+    assert res[0][1] == 0 and sum(r[2] for r in res) == N
+    assert all(r[1] % DECODE == 0 for r in res)
+    # labelled counts: bit-exact vs the unsharded run, on every rank
+    full_i = co.count_labelled(obs, truth, TRAIN)
+    for r in res:
+        assert np.array_equal(r[3], full_i)
+    # E-step: every rank has the same bits = rank-order sum of the parts; ~ unsharded
+    ref_sum = res[0][5].copy()
+    for r in res[1:]:
+        ref_sum += r[5]
+    for r in res:
+        assert np.array_equal(r[4], ref_sum)
+    full_e = co.estep(m, obs, TRAIN)
+    nz = full_e != 0
+    assert np.max(np.abs(ref_sum[nz] - full_e[nz]) / np.abs(full_e[nz])) < 1e-12
+    # islands: the gathered records equal the unsharded decode's, in genome order
+    _, isl, _ = co.decode_chunks(m, obs, DECODE)
+    assert len(isl) > 0
+    for r in res:
+        assert np.array_equal(r[6].view(co.ISLAND_DTYPE), isl)
+    # Baum-Welch over shards: identical models on every rank, ~ the unsharded driver
+    for r in res:
+        assert np.array_equal(r[7], res[0][7]) and r[8] == 3
+    mo = m
+    for _ in range(3):
+        mo = co.normalize(co.estep(mo, obs, TRAIN))
+    assert np.allclose(res[0][7], mo, rtol=1e-11, atol=0)
+
+
+@pytest.mark.parametrize("n,world", [(0, 1), (DECODE - 1, 2), (3 * DECODE, 2),
+                                     (7 * DECODE + 5, 4), (2 * DECODE, 8)])
+def test_shard_bounds_tile(n, world):
+    spans = [cd.shard_bounds(n, world, r, align=DECODE) for r in range(world)]
+    pos = 0
+    for s, ln in spans:
+        assert s == pos and s % DECODE == 0 and ln >= 0
+        pos += ln
+    assert pos == n
+    # whole chunks are balanced within one chunk
+    whole = [ln // DECODE for _, ln in spans]
+    assert max(whole) - min(whole) <= 1 and sum(whole) == n // DECODE
+
+
+def test_single_process_merges_are_identity():
+    t = torch.arange(5, dtype=torch.float64)
+    assert cd.merge_counts_f64(t.clone()).equal(t)
+    assert cd.merge_counts_i64(t.long()).equal(t.long())
+    with pytest.raises(ValueError):
+        cd.shard_bounds(10, 2, 2)

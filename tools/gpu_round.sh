@@ -11,6 +11,13 @@ if [[ $STEPS == *all* || $STEPS == *test* ]]; then
       > $OUT/pytest_gpu.log 2>&1; rc=$?; echo "pytest rc=$rc"; tail -5 $OUT/pytest_gpu.log
   ok $rc || exit $rc
 fi
+if [[ $STEPS == *abl* ]]; then   # E-step timing of each ablation build vs the default build
+  for lib in "" build/abl/*.so; do
+    CPG_LIB_OVERRIDE=$lib timeout -k 10 300 python tools/estep_ablate.py >> $OUT/abl.log 2>&1
+    rc=$?; echo "abl $lib rc=$rc"; [ $rc -eq 0 ] || exit $rc
+  done
+  cat $OUT/abl.log
+fi
 if [[ $STEPS == *all* || $STEPS == *smoke* ]]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $OUT/smoke.log 2>&1
   rc=$?; echo "smoke rc=$rc"; tail -2 $OUT/smoke.log; [ $rc -eq 0 ] || exit $rc
