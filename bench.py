@@ -18,7 +18,9 @@ import os
 import sys
 import time
 
-import torch
+# kernel arguments in device memory (must precede HIP initialisation)
+os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
@@ -69,9 +71,13 @@ def main():
     ap.add_argument("--bases", type=int, default=N_PER_GPU, help="bases per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=8 * DECODE)
+    ap.add_argument("--serial", action="store_true",
+                    help="train and decode phases on one stream (isolated phase timing)")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="write this many MiB of scratch between steps (cold Infinity Cache)")
     args = ap.parse_args()
+    if args.flush_mb:
+        args.serial = True   # the flushed step time is the sum of isolated phase times
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -115,34 +121,51 @@ def main():
     from cpgisland_amd import baumwelch
     model1 = baumwelch.normalize(ecnt.cpu().numpy())
 
-    ev = {k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-          for k in ("estep", "counts", "reduce", "viterbi", "islands")}
-    acc = {k: 0.0 for k in ev}
+    names = ("estep", "counts", "reduce", "viterbi", "islands")
+    # one pair of HIP events per phase per timed step, read after the final synchronize (no
+    # host round trip between steps)
+    evs = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+            for k in names} for _ in range(args.steps)]
+    acc = {k: 0.0 for k in names}
 
-    def step(timed):
+    # The training pass and the decode are independent within a step: by default they run
+    # concurrently on two streams (the decode kernels are latency-bound and leave SIMDs idle
+    # that the E-step fills).  --serial runs everything on one stream (isolated phase times).
+    main_s = torch.cuda.current_stream()
+    s_tr = main_s if args.serial else torch.cuda.Stream()
+    s_dec = main_s if args.serial else torch.cuda.Stream()
+
+    def step(it):
         def mark(k, i):
-            if timed:
-                ev[k][i].record()
-        mark("estep", 0)
-        D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
-        mark("estep", 1)
-        mark("counts", 0)
-        D.count_labelled(ctx, dp, ds, N, TRAIN, out=lcnt)
-        mark("counts", 1)
-        mark("reduce", 0)
-        if dist:   # the reducer: int64 sums are exact in any order; fp64 in rank order
-            cdist.merge_counts_i64(lcnt)
-            cdist.merge_counts_f64(ecnt)
-        mark("reduce", 1)
-        mark("viterbi", 0)
-        D.viterbi(ctx, model1, dp, N, DECODE, sign_out=so, score=score)
-        mark("viterbi", 1)
-        mark("islands", 0)
-        D.islands(ctx, dp, so, N, DECODE, cap=icap, first_chunk=first_chunk, out=iout, count=icnt)
-        mark("islands", 1)
+            if it is not None:
+                evs[it][k][i].record()
+        s_tr.wait_stream(main_s)
+        s_dec.wait_stream(main_s)
+        with torch.cuda.stream(s_dec):
+            mark("viterbi", 0)
+            D.viterbi(ctx, model1, dp, N, DECODE, sign_out=so, score=score)
+            mark("viterbi", 1)
+            mark("islands", 0)
+            D.islands(ctx, dp, so, N, DECODE, cap=icap, first_chunk=first_chunk, out=iout,
+                      count=icnt)
+            mark("islands", 1)
+        with torch.cuda.stream(s_tr):
+            mark("estep", 0)
+            D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
+            mark("estep", 1)
+            mark("counts", 0)
+            D.count_labelled(ctx, dp, ds, N, TRAIN, out=lcnt)
+            mark("counts", 1)
+            mark("reduce", 0)
+            if dist:   # the reducer: int64 sums are exact in any order; fp64 in rank order
+                cdist.merge_counts_i64(lcnt)
+                cdist.merge_counts_f64(ecnt)
+            mark("reduce", 1)
+        main_s.wait_stream(s_tr)
+        main_s.wait_stream(s_dec)
 
     for _ in range(args.warmup):
-        step(False)
+        step(None)
         if flush is not None:
             flush.fill_(1.0)
     torch.cuda.synchronize()
@@ -151,14 +174,14 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
+    for it in range(args.steps):
         if flush is not None:
             flush.fill_(1.0)
-        step(True)
-        torch.cuda.synchronize()
+        step(it)
+    torch.cuda.synchronize()
+    for ev in evs:
         for k, (a, b) in ev.items():
             acc[k] += a.elapsed_time(b)
-    torch.cuda.synchronize()
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -192,6 +215,7 @@ def main():
                                         f"seed {SEED})",
                "config": {"workload": "C2: 46 Mbp chr21-sized per GPU; BW E-step + labelled "
                                       "counts + RCCL reduce + exact Viterbi + islands",
+                          "streams": 1 if args.serial else 2,
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
                           "islands_found": int(icnt.item())},

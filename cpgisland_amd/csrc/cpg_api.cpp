@@ -2,6 +2,7 @@
 // the HBM-resident "_d" entry points and the host-buffer wrappers that mirror the
 // reference call sites (CpGIslandFinder.java:200 training, :260 decode, :262-339 islands).
 
+#include <cstdlib>
 #include <cmath>
 #include <cstring>
 #include <vector>
@@ -21,6 +22,9 @@ int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
         }
         size_t sz = bytes + bytes / 8 + 4096;
         CPG_HIP(hipMalloc(&b.p, sz));
+        // zero-filled once: the count / E-step accumulators rely on it (their final kernels
+        // re-zero them after reading)
+        CPG_HIP(hipMemset(b.p, 0, sz));
         b.bytes = sz;
     }
     *out = b.p;
@@ -95,6 +99,11 @@ extern "C" {
 int cpg_open(int device, cpg_ctx** out) {
     if (!out) return set_error(CPG_E_INVALID, "null out");
     *out = nullptr;
+    // Kernel arguments in device memory instead of host memory: every kernel's first
+    // argument fetch otherwise crosses PCIe (measured ~1 us per launch on MI355X).  Takes
+    // effect only if this is the process's first HIP call (e.g. a JVM host); Python hosts
+    // that initialise HIP through torch first set it in the environment (bench.py).
+    setenv("HIP_FORCE_DEV_KERNARG", "1", 0);
     int n = 0;
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess || n <= 0)
@@ -247,13 +256,15 @@ int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packe
     if (rc) return rc;
     if (chunk_len % 256) return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 256");
     if ((rc = model_check_deterministic(model))) return rc;
+    if (chunk_len % 4096 || chunk_len > 65536)
+        return set_error(CPG_E_INVALID, "E-step chunk_len must be a multiple of 4096, <= 65536");
     std::lock_guard<std::mutex> lk(ctx->mu);
     CPG_HIP(hipSetDevice(ctx->device));
     const int64_t nch = nbases / chunk_len;
     void* ws;
     if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nch, chunk_len), &ws))) return rc;
-    CPG_HIP(launch_estep(*model, d_packed, nch, chunk_len, ws, ctx->ws[WS_EST].bytes,
-                         d_counts, pick(ctx, stream)));
+    CPG_HIP(launch_estep(*model, d_packed, nch, chunk_len, (unsigned long long*)ws, d_counts,
+                         pick(ctx, stream)));
     return CPG_OK;
 }
 

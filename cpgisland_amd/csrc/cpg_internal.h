@@ -107,7 +107,7 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
                           cpg_island* out, int64_t cap, int64_t* count, hipStream_t s);
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
-                        int64_t chunk_len, void* ws, size_t ws_bytes, double* out,
+                        int64_t chunk_len, unsigned long long* acc, double* out,
                         hipStream_t s);
 size_t estep_ws_bytes(int64_t nchunks, int64_t chunk_len);
 

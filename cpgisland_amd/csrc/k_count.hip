@@ -8,9 +8,11 @@
 // inside an island or background run every transition is ++ or --, and only lane-blocks
 // that straddle an island boundary take the general four-class path.
 //
-// Per-workgroup partial counts go to a slab (no global atomics) and a one-workgroup
-// finalize sums the slab in a fixed order and derives emission/dinucleotide/mono counts
-// from the transition + init counts (exact integer identities).
+// Per-workgroup partial counts (and the init states of the chunks starting in the
+// workgroup) are added to 72 global 64-bit accumulators (integer atomics: exact and
+// order-independent, one per counter per workgroup); a one-workgroup finalize derives the
+// emission/dinucleotide/mono counts from the transition + init counts (exact integer
+// identities) and re-zeroes the accumulators.  Two launches per call.
 
 #include "cpg_internal.h"
 
@@ -45,13 +47,18 @@ __device__ __forceinline__ uint32_t spread16(uint32_t x) {
     return x;
 }
 
+__device__ void final_counts(const uint64_t* raw, int t, int64_t* __restrict__ out);
+
 __global__ __launch_bounds__(kCountThreads) void k_count_main(
     const uint4* __restrict__ packed4, const uint2* __restrict__ sign2,
     const uint32_t* __restrict__ packed, const uint32_t* __restrict__ sign, int64_t nblk,
-    int64_t blk_per_chunk, uint64_t* __restrict__ slab) {
+    int64_t blk_per_chunk, unsigned long long* __restrict__ gacc) {
     uint32_t tot[16], pp[16], pm[16], mp[16];
 #pragma unroll
     for (int d = 0; d < 16; ++d) tot[d] = pp[d] = pm[d] = mp[d] = 0u;
+    __shared__ uint32_t sinit[8];   // states of the chunks' first bases (rare: LDS atomics)
+    if (threadIdx.x < 8) sinit[threadIdx.x] = 0u;
+    __syncthreads();
 
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
     for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nblk; i += stride) {
@@ -59,6 +66,7 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
         const uint2 s = sign2[i];
         const bool cstart = (i % blk_per_chunk) == 0;
         uint32_t wprev = 0, sprev = 0;
+        if (cstart) atomicAdd(&sinit[(w.x & 3u) + ((s.x & 1u) ? 0u : 4u)], 1u);
         if (!cstart) {
             wprev = packed[4 * i - 1];
             sprev = sign[2 * i - 1] >> 31;
@@ -147,66 +155,31 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
     __shared__ uint32_t wsum[kCountThreads / 64][64];
     wsum[threadIdx.x >> 6][lane] = v[0];
     __syncthreads();
-    if (threadIdx.x < 64) {
+    if (threadIdx.x < kRaw) {
         uint64_t acc = 0;
+        if (threadIdx.x < 64) {
 #pragma unroll
-        for (int w = 0; w < kCountThreads / 64; ++w) acc += wsum[w][threadIdx.x];
-        slab[(int64_t)threadIdx.x * gridDim.x + blockIdx.x] = acc;   // counter-major
+            for (int w = 0; w < kCountThreads / 64; ++w) acc += wsum[w][threadIdx.x];
+        } else {
+            acc = sinit[threadIdx.x - 64];
+        }
+        if (acc) atomicAdd(gacc + threadIdx.x, (unsigned long long)acc);
     }
 }
 
-// init counts: one thread per chunk, deterministic (no atomics): states of first bases
-__global__ void k_count_init(const uint32_t* __restrict__ packed,
-                             const uint32_t* __restrict__ sign, int64_t nchunks,
-                             int64_t chunk_len, uint32_t* __restrict__ first_state) {
-    int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (c >= nchunks) return;
-    int64_t pos = c * chunk_len;
-    int b = (int)((packed[pos >> 4] >> ((pos & 15) * 2)) & 3u);
-    int s = (int)((sign[pos >> 5] >> (pos & 31)) & 1u);
-    first_state[c] = (uint32_t)(b + (s ? 0 : 4));
-}
-
-// one workgroup per counter: fixed-order tree sum of that counter's per-workgroup partials
-__global__ __launch_bounds__(256) void k_count_reduce(const uint64_t* __restrict__ slab,
-                                                      int nrows, uint64_t* __restrict__ raw) {
-    __shared__ uint64_t s[256];
-    const int t = threadIdx.x;
-    const uint64_t* row = slab + (int64_t)blockIdx.x * nrows;
-    uint64_t acc = 0;
-    for (int r = t; r < nrows; r += 256) acc += row[r];
-    s[t] = acc;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (t < o) s[t] += s[t + o];
-        __syncthreads();
-    }
-    if (t == 0) raw[blockIdx.x] = s[0];
-}
-
-__global__ __launch_bounds__(256) void k_count_final(const uint64_t* __restrict__ raw_in,
-                                                     const uint32_t* __restrict__ first_state,
-                                                     int64_t nchunks, int64_t* __restrict__ out) {
+// One workgroup: the cpg_counts_i64 assembly from the 72 accumulators, which it re-zeroes.
+__global__ __launch_bounds__(128) void k_count_final(unsigned long long* __restrict__ gacc,
+                                                     int64_t* __restrict__ out) {
     __shared__ uint64_t raw[kRaw];
-    __shared__ uint32_t initc[8][256];
     const int t = threadIdx.x;
-    if (t < 64) raw[t] = raw_in[t];
-    uint32_t ic[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    for (int64_t c = t; c < nchunks; c += 256) {
-        const uint32_t fs = first_state[c];
-#pragma unroll
-        for (int k = 0; k < 8; ++k) ic[k] += (fs == (uint32_t)k);
-    }
-#pragma unroll
-    for (int k = 0; k < 8; ++k) initc[k][t] = ic[k];
+    if (t < kRaw) raw[t] = gacc[t];
     __syncthreads();
-    if (t < 8) {
-        uint64_t acc = 0;
-        for (int j = 0; j < 256; ++j) acc += initc[t][j];
-        raw[64 + t] = acc;
-    }
-    __syncthreads();
-    if (t >= 124) return;
+    if (t < kRaw) gacc[t] = 0ull;
+    if (t < 124) final_counts(raw, t, out);
+}
+
+// cpg_counts_i64 from the 72 raw sums (tot | pp | pm | mp | init); thread t < 124
+__device__ void final_counts(const uint64_t* raw, int t, int64_t* __restrict__ out) {
     // cpg_counts_i64 layout: init[8] trans[8][8] emit[8][4] dinuc[4][4] mono[4]; one
     // output word per thread
     int64_t v = 0;
@@ -247,29 +220,16 @@ __global__ __launch_bounds__(256) void k_count_final(const uint64_t* __restrict_
 hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                         int64_t chunk_len, uint64_t* ws, int64_t* out, hipStream_t s) {
     const int64_t nblk = nchunks * chunk_len / 64;
+    if (nblk <= 0) return hipMemsetAsync(out, 0, 124 * sizeof(int64_t), s);
     int grid = 1024;
     if ((int64_t)grid * kCountThreads > nblk) grid = (int)((nblk + kCountThreads - 1) / kCountThreads);
-    if (grid < 1) grid = 1;
-    uint64_t* slab = ws;
-    uint64_t* raw = ws + (size_t)1024 * kRaw;
-    uint32_t* first_state = (uint32_t*)(raw + 128);
-    if (nblk > 0) {
-        hipLaunchKernelGGL(k_count_main, dim3(grid), dim3(kCountThreads), 0, s,
-                           (const uint4*)packed, (const uint2*)sign, packed, sign, nblk,
-                           chunk_len / 64, slab);
-        hipLaunchKernelGGL(k_count_reduce, dim3(64), dim3(256), 0, s, slab, grid, raw);
-    } else {
-        hipMemsetAsync(raw, 0, 64 * sizeof(uint64_t), s);
-    }
-    if (nchunks > 0)
-        hipLaunchKernelGGL(k_count_init, dim3((unsigned)((nchunks + 255) / 256)), dim3(256), 0,
-                           s, packed, sign, nchunks, chunk_len, first_state);
-    hipLaunchKernelGGL(k_count_final, dim3(1), dim3(256), 0, s, raw, first_state, nchunks, out);
+    hipLaunchKernelGGL(k_count_main, dim3(grid), dim3(kCountThreads), 0, s,
+                       (const uint4*)packed, (const uint2*)sign, packed, sign, nblk,
+                       chunk_len / 64, (unsigned long long*)ws);
+    hipLaunchKernelGGL(k_count_final, dim3(1), dim3(128), 0, s, (unsigned long long*)ws, out);
     return hipGetLastError();
 }
 
-size_t count_ws_bytes(int64_t nchunks) {
-    return (size_t)1024 * kRaw * 8 + 128 * 8 + (size_t)(nchunks + 1) * 4;
-}
+size_t count_ws_bytes(int64_t) { return (size_t)kRaw * 8; }
 
 }  // namespace cpg

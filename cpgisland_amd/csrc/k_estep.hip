@@ -18,7 +18,9 @@
 // reciprocal of the sum in the reference) changes results only at rounding level: parity
 // with the oracle is by tolerance (tests: 1e-9 relative).  Emission counts follow exactly
 // from sum_i xi(i,j) = gamma(j): emit[j] = init[j] + column sum j of trans.
-// Per-chunk results go to a slab summed in chunk order: deterministic.
+// Per-chunk results are added to 128-bit fixed-point accumulators (64-bit integer atomics
+// with carry into a high word: exact, order-independent, so deterministic); a
+// one-workgroup finalize converts them to the cpg_counts_f64 stripes.
 
 #include <algorithm>
 #include <cmath>
@@ -40,6 +42,14 @@ constexpr int kSlab = 73;               // trans[64] (by dinucleotide x 4) | ini
 #define EST_KD 1
 #endif
 constexpr int kRep = EST_REP;
+#ifndef EST_NREP
+#define EST_NREP 8
+#endif
+constexpr int kNRep = EST_NREP;   // bin replicas per wave (64 / kNRep lanes share one)
+// LDS: TA/TB (512 B) | union { 4-step tables, scan buffer, bins } | per-wave partials
+constexpr size_t kUnionOff = 32 * 16;
+constexpr size_t kUnionBytes =
+    (size_t)16 * kNRep * kRep * 8 > 2048 * 16 ? (size_t)16 * kNRep * kRep * 8 : 2048 * 16;
 __device__ __forceinline__ int bin_of(int d, int k) { return EST_KD ? k * 16 + d : d * 4 + k; }
 
 struct Mat {
@@ -91,6 +101,16 @@ __device__ __forceinline__ unsigned long long to_fixed_scaled(double y) {   // y
     return (unsigned long long)__double_as_longlong(y + kMagic) -
            (unsigned long long)__double_as_longlong(kMagic);
 }
+constexpr int kLogFix = 24;   // log-likelihood fixed point: 2^-24 (|chunk loglik| < 2^30)
+
+// 128-bit two's-complement accumulation with 64-bit atomics: the adder that wraps the low
+// word carries into the high word (plus the sign extension of a negative addend)
+__device__ __forceinline__ void acc128_add(unsigned long long* lohi, unsigned long long v,
+                                           bool negative) {
+    const unsigned long long old = atomicAdd(lohi, v);
+    const unsigned long long hi = (negative ? ~0ull : 0ull) + (old + v < old ? 1ull : 0ull);
+    if (hi) atomicAdd(lohi + 1, hi);
+}
 
 // the lane's 64 dinucleotide codes (prev | cur << 2), 8 per word, read once from HBM
 struct Codes {
@@ -138,17 +158,22 @@ __device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int
 
 __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
                                                      const uint32_t* __restrict__ packed,
-                                                     int64_t C, double* __restrict__ slab) {
+                                                     int64_t C,
+                                                     unsigned long long* __restrict__ acc) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves
     // conflict-free constant tables: 16 x 16 B each = one 256-B bank row
     double2* TA = reinterpret_cast<double2*>(smem);          // (M(+,+), M(+,-))
     double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
+    // one union region after TA/TB, used in turn by: the 4-step tables (phase 1), the scan
+    // buffer (phase 2), the xi bins (phase 3) — each phase ends with a barrier
     double2* TA4 = TB + 16;                                   // 4-step products, row 0
     double2* TB4 = TA4 + 1024;                                //                  row 1
-    auto* bins = reinterpret_cast<unsigned long long*>(TB4 + 1024);   // [wave][4][kRep]
-    Mat* sm = reinterpret_cast<Mat*>(bins + nw * 4 * kRep);   // [nl] (scan; then checkpoints)
+    Mat* sm = reinterpret_cast<Mat*>(TA4);                    // [nl]
+    auto* bins = reinterpret_cast<unsigned long long*>(TA4);  // [wave][kNRep][kRep]
+    auto* part = reinterpret_cast<unsigned long long*>(
+        smem + kUnionOff + (kUnionBytes > nl * sizeof(Mat) ? kUnionBytes : nl * sizeof(Mat)));
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int64_t c = blockIdx.x;
@@ -158,7 +183,6 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         TA[t] = make_double2(model.a[p][b], model.a[p][b + 4]);
         TB[t] = make_double2(model.a[p + 4][b], model.a[p + 4][b + 4]);
     }
-    for (int i = t; i < nw * 4 * kRep; i += nl) bins[i] = 0ull;
     // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4)
     for (int i = t; i < 1024; i += nl) {
         int b[5];
@@ -186,6 +210,7 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     // 1. lane product of M_p over its positions, four matrices per lookup (position 0
     //    carries no matrix: lane 0's first group is M_1 M_2 M_3)
     Mat P = mid();
+    Mat Pm[NMB - 1];   // products after mini-blocks 0 .. NMB-2: the alpha checkpoints
 #pragma unroll
     for (int gq = 0; gq < L / 4; ++gq) {
         double2 ra, rb;
@@ -211,7 +236,9 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
               P.c * ra.y + P.d * rb.y, P.e};
         P = r;
         if ((gq & 1) == 1) mnorm(P);
+        if ((gq & 3) == 3 && gq / 4 < NMB - 1) Pm[gq / 4] = P;
     }
+    __syncthreads();   // the 4-step tables are dead from here: the scan buffer reuses them
     // 2a. inclusive prefix (Hillis-Steele)
     sm[t] = P;
     __syncthreads();
@@ -239,6 +266,16 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         aM = fb;
     }
     vnorm(aP, aM);
+    double fcP[NMB], fcM[NMB];   // the alpha checkpoints (see 3a)
+    fcP[0] = aP;
+    fcM[0] = aM;
+#pragma unroll
+    for (int m = 1; m < NMB; ++m) {
+        const Mat& A = Pm[m - 1];
+        fcP[m] = aP * A.a + aM * A.c;
+        fcM[m] = aP * A.b + aM * A.d;
+        vnorm(fcP[m], fcM[m]);
+    }
     __syncthreads();
     // 2b. inclusive suffix
     sm[t] = P;
@@ -259,33 +296,26 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     vnorm(bP, bM);
     __syncthreads();
 
-    // 3a. backward checkpoints: beta at the last position of each mini-block ([m][lane] in
-    //     LDS, aliasing the scan buffer: 16-B rows, conflict-free)
-    double2* ck = reinterpret_cast<double2*>(sm);
-    {
-        double xP = bP, xM = bM;
-#pragma unroll
-        for (int m = NMB - 1; m >= 0; --m) {
-            ck[m * nl + t] = make_double2(xP, xM);
-            if (m == 0) break;
-#pragma unroll
-            for (int gq = 4 * m + 3; gq >= 4 * m; --gq) {   // beta_{4g-1} = T4(g) beta_{4g+3}
-                const uint32_t wi = cd.win(gq);
-                const double2 ra = TA4[wi], rb = TB4[wi];
-                const double nP = ra.x * xP + ra.y * xM, nM = rb.x * xP + rb.y * xM;
-                xP = nP;
-                xM = nM;
-            }
-            vnorm(xP, xM);
-        }
-    }
-    // 3b. mini-blocks: forward alphas in registers, then backward with xi accumulation
-    unsigned long long* wb = bins + ((t >> 6) * 4 + (lane >> 4)) * kRep;   // 16-lane replica
+    // 3a. bins (aliasing the scan buffer, read above) zeroed; alpha entering mini-block m
+    //     = alpha entering the lane times phase 1's product of the first m mini-blocks
+    //     (any per-position scale cancels in the normalised xi)
+    for (int i = t; i < nw * kNRep * kRep; i += nl) bins[i] = 0ull;
+    __syncthreads();
+    // 3b. mini-blocks, last to first: forward alphas in registers from the checkpoint, then
+    //     backward with xi accumulation; beta flows on from one mini-block to the previous
+    unsigned long long* wb = bins + ((t >> 6) * kNRep + lane / (64 / kNRep)) * kRep;
     double g0P = 0.0, g0M = 0.0;
-    double bfP = aP, bfM = aM;   // alpha at the position before the mini-block
+    double yP = bP, yM = bM;   // beta at the last position of the mini-block
 #pragma unroll 1
-    for (int m = 0; m < NMB; ++m) {
+    for (int m = NMB - 1; m >= 0; --m) {
         const uint64_t cm = cd.mb(m);
+        // alpha at the position before the mini-block (select chain: no register indexing)
+        double bfP = fcP[0], bfM = fcM[0];
+#pragma unroll
+        for (int k = 1; k < NMB; ++k) {
+            bfP = m == k ? fcP[k] : bfP;
+            bfM = m == k ? fcM[k] : bfM;
+        }
         double alP[kMB], alM[kMB];
         double xP = bfP, xM = bfM;
 #pragma unroll
@@ -304,8 +334,6 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             alP[i] = xP;
             alM[i] = xM;
         }
-        const double2 cz = ck[m * nl + t];
-        double yP = cz.x, yM = cz.y;
 #pragma unroll
         for (int i = kMB - 1; i >= 0; --i) {
             if (t == 0 && m == 0 && i == 0) {   // gamma_0 -> init counts
@@ -330,48 +358,59 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             yM = nM;
             if ((i & 3) == 0) vnorm(yP, yM);
         }
-        bfP = alP[kMB - 1];
-        bfM = alM[kMB - 1];
     }
     __syncthreads();
-    // slab is counter-major: [kSlab][nchunks]
-    const int64_t nch = gridDim.x;
-    if (t < 64) {   // slab row t = d * 4 + k
+    // chunk totals of the nw * kNRep replicas: wave q sums replicas q, q + nw, ... of every
+    // bin (integer sums: exact in any order), then 64 lanes add the nw partials
+    {
+        const int q = t >> 6, b = bin_of(lane >> 2, lane & 3);   // lane = slab row d*4+k
         unsigned long long s = 0;
-        const int b = bin_of(t >> 2, t & 3);
-        for (int r = 0; r < nw * 4; ++r) s += bins[r * kRep + b];
-        slab[t * nch + c] = (double)s * (1.0 / kFix);
+        for (int r = q; r < nw * kNRep; r += nw) s += bins[r * kRep + b];
+        part[q * 64 + lane] = s;
+    }
+    __syncthreads();
+    // chunk results -> the global 128-bit accumulators: xi bins and the init posteriors in
+    // 2^-47 units, the log-likelihood in signed 2^-24 units
+    if (t < 64) {   // row t = d * 4 + k
+        unsigned long long s = 0;
+        for (int q = 0; q < nw; ++q) s += part[q * 64 + t];
+        acc128_add(acc + 2 * t, s, false);
     }
     if (t == 0) {
-        for (int i = 0; i < 8; ++i) slab[(64 + i) * nch + c] = 0.0;
-        slab[(64 + o0) * nch + c] = g0P;
-        slab[(64 + o0 + 4) * nch + c] = g0M;
+        acc128_add(acc + 2 * (64 + o0), to_fixed_scaled(g0P * kFix), false);
+        acc128_add(acc + 2 * (64 + o0 + 4), to_fixed_scaled(g0M * kFix), false);
     }
-    if (t == nl - 1) slab[72 * nch + c] = loglik;
+    if (t == nl - 1) {
+        const long long L = llrint(ldexp(loglik, kLogFix));
+        acc128_add(acc + 2 * 72, (unsigned long long)L, L < 0);
+    }
 }
 
-// one workgroup per counter: fixed-order tree sum over chunks (deterministic)
-__global__ __launch_bounds__(256) void k_estep_reduce(const double* __restrict__ slab,
-                                                      int64_t nchunks, double* __restrict__ v) {
-    __shared__ double s[256];
-    const int t = threadIdx.x;
-    const double* row = slab + (int64_t)blockIdx.x * nchunks;
-    double acc = 0.0;
-    for (int64_t c = t; c < nchunks; c += 256) acc += row[c];
-    s[t] = acc;
-    __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-        if (t < o) s[t] += s[t + o];
-        __syncthreads();
-    }
-    if (t == 0) v[blockIdx.x] = s[0];
-}
+__device__ void final_estep(const double* v, int t, double* __restrict__ out);
 
-__global__ __launch_bounds__(128) void k_estep_final(const double* __restrict__ v,
+// One workgroup: the 73 accumulators -> doubles (re-zeroed for the next call), then the
+// cpg_counts_f64 assembly.
+__global__ __launch_bounds__(256) void k_estep_final(unsigned long long* __restrict__ acc,
                                                      double* __restrict__ out) {
-    // cpg_counts_f64: init[8] trans[8][8] emit[8][4] loglik; one output per thread
+    __shared__ double vsum[kSlab];
     const int t = threadIdx.x;
-    if (t >= 105) return;
+    if (t < kSlab) {
+        unsigned long long lo = acc[2 * t], hi = acc[2 * t + 1];
+        const bool neg = (long long)hi < 0;   // only the log-likelihood row can be negative
+        if (neg) {                             // magnitude first: no cancellation
+            lo = ~lo + 1ull;
+            hi = ~hi + (lo == 0ull ? 1ull : 0ull);
+        }
+        const double mag = (double)hi * 18446744073709551616.0 + (double)lo;
+        vsum[t] = t < 72 ? mag * (1.0 / kFix) : ldexp(neg ? -mag : mag, -kLogFix);
+    }
+    __syncthreads();
+    if (t < 2 * kSlab) acc[t] = 0ull;
+    if (t < 105) final_estep(vsum, t, out);
+}
+
+// cpg_counts_f64 from the 73 sums: init[8] trans[8][8] emit[8][4] loglik; thread t < 105
+__device__ void final_estep(const double* v, int t, double* __restrict__ out) {
     double r = 0.0;
     if (t < 8) {
         r = v[64 + t];
@@ -396,25 +435,19 @@ __global__ __launch_bounds__(128) void k_estep_final(const double* __restrict__ 
 
 }  // namespace
 
-size_t estep_ws_bytes(int64_t nchunks, int64_t) { return (size_t)(nchunks + 1) * kSlab * 8 + 4096; }
+size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8; }
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
-                        int64_t C, void* ws, size_t ws_bytes, double* out, hipStream_t s) {
-    if (estep_ws_bytes(nchunks, C) > ws_bytes) return hipErrorInvalidValue;
+                        int64_t C, unsigned long long* acc, double* out, hipStream_t s) {
     if (C % 4096 || C > (int64_t)kET * kLanePos) return hipErrorInvalidValue;
+    if (nchunks == 0) return hipMemsetAsync(out, 0, 105 * sizeof(double), s);
     const int lanes = (int)(C / kLanePos);
-    double* slab = static_cast<double*>(ws);
-    const size_t lds = (32 + 2048) * sizeof(double2) + (size_t)(lanes / 64) * 4 * kRep * sizeof(double) +
-                       std::max(lanes * sizeof(Mat), (size_t)lanes * (kLanePos / 16) * 16);
-    if (nchunks > 0)
-        hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
-                           packed, C, slab);
-    double* v = slab + (size_t)(nchunks + 1) * kSlab;
-    if (nchunks > 0)
-        hipLaunchKernelGGL(k_estep_reduce, dim3(kSlab), dim3(256), 0, s, slab, nchunks, v);
-    else if (hipMemsetAsync(v, 0, kSlab * sizeof(double), s) != hipSuccess)
-        return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(128), 0, s, v, out);
+    // the union is sized for 16 waves; a smaller chunk (fewer lanes) uses a prefix of it
+    const size_t uni = std::max(kUnionBytes, (size_t)lanes * sizeof(Mat));
+    const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long);
+    hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
+                       packed, C, acc);
+    hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);
     return hipGetLastError();
 }
 

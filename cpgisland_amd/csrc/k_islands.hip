@@ -12,8 +12,9 @@
 // scan over the chunk's islands.  Islands still open at the chunk end are dropped (:269-339
 // never closes them).  Coordinates and (cgCount*islandLen) use Java int arithmetic.
 //
-// Kernels: IA (per chunk) run boundaries + word prefixes; IB (per chunk) per-run stats,
-// stale scan, filter, kept rank; IC (one workgroup) chunk offsets; ID (per chunk) records.
+// Kernels: A1 (per 1024-word tile) tile totals; A3 (per tile) word prefixes + run
+// boundaries, offset = sum of earlier tiles; B (per chunk) per-run stats, stale scan, filter,
+// kept rank; D (per chunk) records at offset = kept islands of earlier chunks.
 
 #include "cpg_internal.h"
 
@@ -117,7 +118,6 @@ struct IslWs {
     int32_t* nruns;     // per chunk
     int32_t* ncloses;
     int64_t* nkept;
-    int64_t* off;
     void* tiles;        // Cnt5 per (chunk, tile)
     size_t bytes;
 };
@@ -142,7 +142,6 @@ IslWs carve_isl(void* base, int64_t nchunks, int64_t C) {
     w.nruns = (int32_t*)take(nchunks * 4);
     w.ncloses = (int32_t*)take(nchunks * 4);
     w.nkept = (int64_t*)take(nchunks * 8);
-    w.off = (int64_t*)take((nchunks + 1) * 8);
     w.tiles = take(nchunks * ((nw + 1023) / 1024) * 20 + 16);
     w.bytes = o + 256;
     return w;
@@ -201,20 +200,6 @@ __global__ __launch_bounds__(kAT) void k_isl_a1(const uint32_t* packed, const ui
     if (threadIdx.x == 0) tiles[blockIdx.x] = tot;
 }
 
-// A2: per chunk, exclusive scan of its tile totals (in place) + run counts
-__global__ __launch_bounds__(64) void k_isl_a2(int ntiles, Cnt5* __restrict__ tiles, IslWs ws) {
-    const int64_t c = blockIdx.x;
-    if (threadIdx.x != 0) return;
-    Cnt5 acc{0, 0, 0, 0, 0};
-    for (int i = 0; i < ntiles; ++i) {
-        const Cnt5 x = tiles[c * ntiles + i];
-        tiles[c * ntiles + i] = acc;
-        acc = cadd(acc, x);
-    }
-    ws.nruns[c] = acc.st;
-    ws.ncloses[c] = acc.cl;
-}
-
 // A3: word prefixes and run boundaries
 __global__ __launch_bounds__(kAT) void k_isl_a3(const uint32_t* packed, const uint32_t* sign,
                                                int64_t C, int ntiles,
@@ -232,8 +217,15 @@ __global__ __launch_bounds__(kAT) void k_isl_a3(const uint32_t* packed, const ui
     for (int i = 0; i < 4; ++i)
         if (w0 + i < nw) s = cadd(s, cnt_of(m[i]));
     __shared__ Cnt5 sb[kAT];
-    Cnt5 tot;
-    Cnt5 e = cadd(block_scan(s, sb, tot), tiles[blockIdx.x]);
+    // this tile's offset in the chunk: the sum of the earlier tiles' A1 totals
+    Cnt5 before{0, 0, 0, 0, 0}, off, tot;
+    for (int i = threadIdx.x; i < tile; i += kAT) before = cadd(before, tiles[c * ntiles + i]);
+    block_scan(before, sb, off);
+    Cnt5 e = cadd(block_scan(s, sb, tot), off);
+    if (tile == ntiles - 1 && threadIdx.x == 0) {   // chunk totals: runs opened / closed
+        ws.nruns[c] = off.st + tot.st;
+        ws.ncloses[c] = off.cl + tot.cl;
+    }
     int32_t* Cp = ws.Cp + c * nw;
     int32_t* Gp = ws.Gp + c * nw;
     int32_t* CGp = ws.CGp + c * nw;
@@ -375,34 +367,24 @@ __global__ __launch_bounds__(kIT) void k_isl_b(const uint32_t* packed, const uin
     if (t == kIT - 1) ws.nkept[c] = sK[kIT - 1];
 }
 
-__global__ __launch_bounds__(kIT) void k_isl_c(int64_t nchunks, IslWs ws, int64_t* count) {
-    const int t = threadIdx.x;
-    const int64_t per = (nchunks + kIT - 1) / kIT;
-    const int64_t c0 = min((int64_t)t * per, nchunks), c1 = min(c0 + per, nchunks);
-    int64_t s = 0;
-    for (int64_t c = c0; c < c1; ++c) s += ws.nkept[c];
-    __shared__ int64_t sb[kIT];
-    sb[t] = s;
-    __syncthreads();
-    for (int off = 1; off < kIT; off <<= 1) {
-        int64_t x = sb[t];
-        if (t >= off) x += sb[t - off];
-        __syncthreads();
-        sb[t] = x;
-        __syncthreads();
-    }
-    int64_t o = t > 0 ? sb[t - 1] : 0;
-    for (int64_t c = c0; c < c1; ++c) {
-        ws.off[c] = o;
-        o += ws.nkept[c];
-    }
-    if (t == kIT - 1) *count = sb[kIT - 1];
-}
-
 __global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, const uint32_t* sign,
                                                int64_t C, int64_t first_chunk, IslWs ws,
-                                               cpg_island* out, int64_t cap) {
+                                               cpg_island* out, int64_t cap, int64_t* count) {
     const int64_t c = blockIdx.x;
+    // the chunk's first record: kept islands of all earlier chunks (fixed-order sum)
+    __shared__ int64_t sb[kIT];
+    {
+        int64_t a = 0;
+        for (int64_t i = threadIdx.x; i < c; i += kIT) a += ws.nkept[i];
+        sb[threadIdx.x] = a;
+        __syncthreads();
+        for (int o = kIT / 2; o > 0; o >>= 1) {
+            if ((int)threadIdx.x < o) sb[threadIdx.x] += sb[threadIdx.x + o];
+            __syncthreads();
+        }
+    }
+    const int64_t base = sb[0];
+    if (c == (int64_t)gridDim.x - 1 && threadIdx.x == 0) *count = base + ws.nkept[c];
     const int64_t nw = C / 32, maxr = C / 2 + 1;
     const uint32_t* pk = packed + c * (C / 16);
     const uint32_t* sg = sign + c * nw;
@@ -415,7 +397,7 @@ __global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, const uin
     for (int64_t r = threadIdx.x; r < nr; r += kIT) {
         const int32_t k = kept[r];
         if (k < 0) continue;
-        const int64_t dst = ws.off[c] + (k >> 1);
+        const int64_t dst = base + (k >> 1);
         if (dst >= cap) continue;
         const RunStat rs = run_stat(pk, sg, ws, c, nw, st[r], cl[r]);
         const Rec o = filter(rs, (uint32_t)(k & 1));
@@ -446,14 +428,12 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
     Cnt5* tiles = static_cast<Cnt5*>(ws.tiles);
     hipLaunchKernelGGL(k_isl_a1, dim3((unsigned)(nchunks * ntiles)), dim3(kAT), 0, s, packed,
                        sign, chunk_len, ntiles, tiles);
-    hipLaunchKernelGGL(k_isl_a2, dim3((unsigned)nchunks), dim3(64), 0, s, ntiles, tiles, ws);
     hipLaunchKernelGGL(k_isl_a3, dim3((unsigned)(nchunks * ntiles)), dim3(kAT), 0, s, packed,
                        sign, chunk_len, ntiles, tiles, ws);
     hipLaunchKernelGGL(k_isl_b, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
                        chunk_len, ws);
-    hipLaunchKernelGGL(k_isl_c, dim3(1), dim3(kIT), 0, s, nchunks, ws, count);
     hipLaunchKernelGGL(k_isl_d, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
-                       chunk_len, first_chunk, ws, out, cap);
+                       chunk_len, first_chunk, ws, out, cap, count);
     return hipGetLastError();
 }
 

@@ -20,7 +20,7 @@
 //   K1 approx composite   int32 fixed-point 2x2 composite per block
 //   K2 plan               per chunk: scan of K1 composites -> approximate values at every
 //                         block boundary (error <= eps, bounded on the host); classify each
-//                         block: REGULAR (inside one binade), SPLIT (one binade crossing:
+//                         block (same kernel): REGULAR (inside one binade), SPLIT (one binade crossing:
 //                         exact prefix composite + short sequential window + exact suffix
 //                         composite), SEQ (sequential), DEGEN (pi = 0 for both live states)
 //   K3/K3b exact composite fp64 composites with the binade-rounded constants (exact)
@@ -165,7 +165,7 @@ __device__ __forceinline__ BlockWords load_block(const uint32_t* __restrict__ pk
     BlockWords b;
     const uint4* p4 = reinterpret_cast<const uint4*>(pk + wbase);
     const uint4 a0 = p4[0], a1 = p4[1], a2 = p4[2], a3 = p4[3];
-    b.prev = pk[wbase - 1];
+    b.prev = k > 0 ? pk[wbase - 1] : 0u;   // block 0: no word before (its step 0 is skipped)
     b.w[0] = a0.x; b.w[1] = a0.y; b.w[2] = a0.z; b.w[3] = a0.w;
     b.w[4] = a1.x; b.w[5] = a1.y; b.w[6] = a1.z; b.w[7] = a1.w;
     b.w[8] = a2.x; b.w[9] = a2.y; b.w[10] = a2.z; b.w[11] = a2.w;
@@ -201,6 +201,8 @@ __device__ __forceinline__ void pipelined(Idx&& idx, Fetch&& fetch, Use&& use) {
 struct Geo {
     int64_t nchunks, C, nsb;
     __device__ __forceinline__ bool full(int64_t k) const { return k > 0 && (k + 1) * kSB <= C; }
+    // all 256 positions inside the chunk (block 0 included: its step 0 is an identity)
+    __device__ __forceinline__ bool whole(int64_t k) const { return (k + 1) * kSB <= C; }
     __device__ __forceinline__ int jfirst(int64_t k) const { return k == 0 ? 1 : 0; }
     __device__ __forceinline__ int jend(int64_t k) const {
         int64_t e = C - k * kSB;
@@ -222,19 +224,75 @@ __device__ __forceinline__ int4 i4_mul(const int4 a, const int4 b) {   // max-pl
 // -->+, +->-, -->-)
 __device__ __forceinline__ int4 q_mat(const int4 q) { return make_int4(q.x, q.z, q.y, q.w); }
 
+// Block 0 of every chunk starts at the chunk's first base and crosses several binades
+// (|delta| grows from ~2 to ~360 over its 256 steps), so it is always walked sequentially.
+// That walk needs nothing but the bases and the model: K1's extra "head" workgroups run it
+// (one lane per chunk, the reference step with the original constants, pipelined table
+// lookups) while the main workgroups build composites; K4 starts from its exit value.
+__device__ void vit_head(const VitConsts& vc, const uint32_t* packed, const Geo& g,
+                         int64_t c, double2* __restrict__ vhead) {
+    __shared__ double2 HA[17], HB[17];   // (l0, l1) | (l2, l3); entry 16: identity step
+    if (threadIdx.x < 16) {
+        HA[threadIdx.x] = make_double2(vc.L[threadIdx.x][0], vc.L[threadIdx.x][1]);
+        HB[threadIdx.x] = make_double2(vc.L[threadIdx.x][2], vc.L[threadIdx.x][3]);
+    } else if (threadIdx.x == 16) {
+        HA[16] = make_double2(0.0, -INFINITY);
+        HB[16] = make_double2(-INFINITY, 0.0);
+    }
+    __syncthreads();
+    if (c >= g.nchunks) return;
+    const uint32_t* pk = chunk_ptr(packed, g, c);
+    const uint32_t o0 = pk[0] & 3u;
+    double P = vc.logpi[o0], M = vc.logpi[o0 + 4];
+    if (g.whole(0)) {
+        const BlockWords bw = load_block(pk, 0);
+        pipelined<4, kSB>([&](int j) { return j == 0 ? 16u : bw_code(bw, j); },
+                          [&](uint32_t d) { return C64{HA[d].x, HA[d].y, HB[d].x, HB[d].y}; },
+                          [&](const C64& l, int) {
+                              const Step st = ref_step(P, M, l.pp, l.pm, l.mp, l.mm);
+                              P = st.P;
+                              M = st.M;
+                          });
+    } else {
+        walk_block<false>(pk, 0, g.C, [&](uint32_t d, int, int) {
+            const Step st = ref_step(P, M, HA[d].x, HA[d].y, HB[d].x, HB[d].y);
+            P = st.P;
+            M = st.M;
+        });
+    }
+    vhead[c] = make_double2(P, M);
+}
+
 __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uint32_t* packed,
-                                                         Geo g, int4* __restrict__ comp) {
+                                                         Geo g, int4* __restrict__ comp,
+                                                         unsigned main_grid,
+                                                         double2* __restrict__ vhead) {
+    if (blockIdx.x >= main_grid) {   // workgroup-uniform: head workgroups
+        vit_head(vc, packed, g, (int64_t)(blockIdx.x - main_grid) * kThreads + threadIdx.x,
+                 vhead);
+        return;
+    }
     __shared__ int4 Q[16];
-    __shared__ int4 Q4[1024];   // 4-step products over 5-base windows (exact: integers)
+    // 4-step products over 5-base windows b0..b4 (exact: integers) [0, 1024), then the
+    // 3-step products of steps 1..3 over b1..b4 [1024, 1280): block 0's first window (the
+    // chunk's position 0 carries no step)
+    __shared__ int4 Q4[1280];
     if (threadIdx.x < 16)
         Q[threadIdx.x] = make_int4(vc.Q[threadIdx.x][0], vc.Q[threadIdx.x][1],
                                    vc.Q[threadIdx.x][2], vc.Q[threadIdx.x][3]);
     __syncthreads();
-    for (int i = threadIdx.x; i < 1024; i += kThreads) {
-        int4 m = q_mat(Q[(i & 3) | (((i >> 2) & 3) << 2)]);
+#ifndef VIT_ABL_K1   // development ablations (tools/build_ablations.sh); product: undefined
+#define VIT_ABL_K1 0
+#endif
+    for (int i = threadIdx.x; i < 1280; i += kThreads) {
+        if (VIT_ABL_K1 == 1) { Q4[i] = make_int4(i, -i, 3 * i, i >> 2); continue; }
+        const bool three = i >= 1024;
+        const int w = three ? (i - 1024) << 2 : i;   // b0 = 0 unused for the 3-step entries
+        int4 m = three ? make_int4(0, kNeg32, kNeg32, 0)
+                       : q_mat(Q[(w & 3) | (((w >> 2) & 3) << 2)]);
 #pragma unroll
         for (int k = 1; k < 4; ++k) {
-            const int p = (i >> (2 * k)) & 3, b = (i >> (2 * k + 2)) & 3;
+            const int p = (w >> (2 * k)) & 3, b = (w >> (2 * k + 2)) & 3;
             m = i4_mul(m, q_mat(Q[p | (b << 2)]));
         }
         Q4[i] = m;
@@ -244,15 +302,21 @@ __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uin
     if (gid >= g.nchunks * g.nsb) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     const uint32_t* pk = chunk_ptr(packed, g, c);
-    if (g.full(k)) {
+    if (VIT_ABL_K1 == 2) {
+        comp[gid] = Q4[gid & 1023];
+        return;
+    }
+    if (g.whole(k)) {
         int4 acc = make_int4(0, kNeg32, kNeg32, 0);
         const BlockWords bw = load_block(pk, k);
+        const bool first = k == 0;
         pipelined<4, 64>(
             [&](int j) {   // 5-base window of steps 4j .. 4j+3
                 const int r = j >> 2, s = j & 3;
                 const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
-                return s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 0x3FFu)
-                              : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
+                const uint32_t wi = s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 0x3FFu)
+                                           : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
+                return (j == 0 && first) ? 1024u + (wi >> 2) : wi;
             },
             [&](uint32_t wi) { return Q4[wi]; }, [&](const int4 q, int) { acc = i4_mul(acc, q); });
         comp[gid] = acc;
@@ -278,26 +342,59 @@ __device__ __forceinline__ bool binade_ok(const VitConsts& vc, int e) {
     return e >= vc.emin && e <= vc.emax && !((vc.tie_mask >> e) & 1ull);
 }
 
-// K2a: per chunk (1024 lanes): scan of the K1 composites -> approximate value entering
-// every block (fixed point, int64); aent[nsb] = value after the last block.
+// K2 (one workgroup of 1024 lanes per chunk): scan of the K1 composites -> approximate
+// value entering every block (fixed point, int64; aent[nsb] = value after the last block),
+// then every block is classified from its entry/exit estimates: REGULAR (inside one
+// binade) or irregular (listed for K3b); block 0 is always sequential; DEGEN chunks (pi = 0
+// for both live states) skip everything.
 constexpr int kScanT = 1024;
+__device__ __forceinline__ VitPlan classify(const VitConsts& vc, const Geo& g, int64_t k,
+                                            longlong2 en, longlong2 ex, bool& irregular) {
+    const double invS = ldexp(1.0, -vc.qshift);
+    VitPlan p{PLAN_SEQ, 0, 0, 0, 0, 0};
+    const int j0 = g.jfirst(k), jend = g.jend(k);
+    irregular = false;
+    if (k > 0 && jend > j0) {
+        const double hi = (double)mx(en.x, en.y) * invS + vc.eps;
+        const double lo = (double)mx(ex.x, ex.y) * invS - vc.eps - vc.spread;
+        const int e = hi < 0.0 ? ilogb(-hi) : -1;
+        if (e >= 0 && binade_ok(vc, e) && lo > -ldexp(1.0, e + 1))
+            p = VitPlan{PLAN_REGULAR, (int8_t)e, 0, 0, (uint16_t)jend, (uint16_t)jend};
+        else
+            irregular = hi < 0.0;
+    }
+    return p;
+}
+
 __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_t* packed, Geo g,
                                                      const int4* __restrict__ comp,
                                                      longlong2* __restrict__ aent,
-                                                     uint8_t* __restrict__ degen) {
+                                                     uint8_t* __restrict__ degen,
+                                                     VitPlan* __restrict__ plan,
+                                                     int32_t* __restrict__ irrlist,
+                                                     int32_t* __restrict__ irrcount) {
     const int64_t c = blockIdx.x;
     const int t = threadIdx.x;
     const uint32_t* pk = chunk_ptr(packed, g, c);
     const int4* cc = comp + c * g.nsb;
     longlong2* ae = aent + c * (g.nsb + 1);
+    VitPlan* pl = plan + c * g.nsb;
     __shared__ CI buf[kScanT];
+    __shared__ int sIrr;
     const int64_t per = (g.nsb + kScanT - 1) / kScanT;
     const int64_t b0 = min((int64_t)t * per, g.nsb), b1 = min(b0 + per, g.nsb);
     const uint32_t o0 = base_at(pk, 0);
     const double lp = vc.logpi[o0], lm = vc.logpi[o0 + 4];
-    const bool dg = !(lp > -INFINITY) && !(lm > -INFINITY);
-    if (t == 0) degen[c] = dg ? 1 : 0;
-    if (dg) return;
+    const bool dg = !(lp > -INFINITY) && !(lm > -INFINITY);   // uniform per workgroup
+    if (t == 0) {
+        degen[c] = dg ? 1 : 0;
+        sIrr = 0;
+    }
+    if (dg) {
+        for (int64_t k = b0; k < b1; ++k) pl[k] = VitPlan{PLAN_DEGEN, 0, 0, 0, 0, 0};
+        if (t == 0) irrcount[c] = 0;
+        return;
+    }
     CI prod = ci_id();
     for (int64_t k = b0; k < b1; ++k) {
         const int4 x = cc[k];
@@ -316,44 +413,17 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
     int64_t P = fix_of(lp, f), M = fix_of(lm, f);
     if (t > 0) ci_apply(P, M, buf[t - 1]);
     for (int64_t k = b0; k < b1; ++k) {
-        ae[k] = make_longlong2(P, M);
+        const longlong2 en = make_longlong2(P, M);
+        ae[k] = en;
         const int4 x = cc[k];
         ci_apply(P, M, CI{x.x, x.y, x.z, x.w});
+        bool irregular;
+        pl[k] = classify(vc, g, k, en, make_longlong2(P, M), irregular);
+        if (irregular) irrlist[c * g.nsb + atomicAdd(&sIrr, 1)] = (int32_t)k;
     }
     if (b1 == g.nsb && b0 < b1) ae[g.nsb] = make_longlong2(P, M);
-}
-
-// K2b: one lane per block: REGULAR (inside one binade) or irregular (listed for K3b);
-// block 0 is always sequential; DEGEN chunks skip everything
-__global__ __launch_bounds__(kThreads) void k_vit_classify(
-    VitConsts vc, Geo g, const longlong2* __restrict__ aent, const uint8_t* __restrict__ degen,
-    VitPlan* __restrict__ plan, int32_t* __restrict__ irrlist, int32_t* __restrict__ irrcount) {
-    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (gid >= g.nchunks * g.nsb) return;
-    const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
-    if (degen[c]) {
-        plan[gid] = VitPlan{PLAN_DEGEN, 0, 0, 0, 0, 0};
-        return;
-    }
-    const longlong2 en = aent[c * (g.nsb + 1) + k], ex = aent[c * (g.nsb + 1) + k + 1];
-    const double invS = ldexp(1.0, -vc.qshift);
-    VitPlan p{PLAN_SEQ, 0, 0, 0, 0, 0};
-    const int j0 = g.jfirst(k), jend = g.jend(k);
-    bool irregular = false;
-    if (k > 0 && jend > j0) {
-        const double hi = (double)mx(en.x, en.y) * invS + vc.eps;
-        const double lo = (double)mx(ex.x, ex.y) * invS - vc.eps - vc.spread;
-        const int e = hi < 0.0 ? ilogb(-hi) : -1;
-        if (e >= 0 && binade_ok(vc, e) && lo > -ldexp(1.0, e + 1))
-            p = VitPlan{PLAN_REGULAR, (int8_t)e, 0, 0, (uint16_t)jend, (uint16_t)jend};
-        else
-            irregular = hi < 0.0;
-    }
-    plan[gid] = p;
-    if (irregular) {
-        const int slot = atomicAdd(irrcount + c, 1);
-        irrlist[c * g.nsb + slot] = (int32_t)k;
-    }
+    __syncthreads();
+    if (t == 0) irrcount[c] = sIrr;
 }
 
 // ---------------------------------------------------------------- K3: exact composites
@@ -606,7 +676,8 @@ __device__ __forceinline__ void st_c64(double4* p, const C64& c) {
 // depend on the chain, so they issue ahead of it.
 constexpr int kChainT = 1024;
 constexpr int kMaxStagedBar = 64;     // barriers staged in LDS per chunk
-constexpr int kStageSteps = 1536;     // window steps staged in LDS per chunk
+constexpr int kStageSteps = 512;      // window steps staged in LDS per chunk (block 0
+                                      // is walked by K1's head lanes, not here)
 __device__ __forceinline__ double2 chain_window(const uint32_t* __restrict__ pk,
                                                 const double4* sL, double4* stepL, int64_t k,
                                                 int ja, int jb, double2 v, int lane) {
@@ -633,11 +704,17 @@ __device__ __forceinline__ double2 chain_window(const uint32_t* __restrict__ pk,
     return make_double2(__shfl(P, 0), __shfl(M, 0));
 }
 
+#ifdef CPG_DEBUG_CHAIN
+#define CPG_CHAIN_MARK(n) const unsigned long long n = wall_clock64();
+#else
+#define CPG_CHAIN_MARK(n)
+#endif
 __global__ __launch_bounds__(kChainT) void k_vit_chain(
     VitConsts vc, const uint32_t* packed, Geo g, const VitPlan* __restrict__ plan,
     const double4* __restrict__ comp3, const uint8_t* __restrict__ degen,
     double2* __restrict__ entry, double4* __restrict__ gk, double4* __restrict__ gap,
-    int32_t* __restrict__ barlist, double2* __restrict__ vout) {
+    int32_t* __restrict__ barlist, double2* __restrict__ vout,
+    const double2* __restrict__ vhead) {
     const int64_t c = blockIdx.x;
     const int t = threadIdx.x;
     const int64_t per = (g.nsb + kChainT - 1) / kChainT;
@@ -660,49 +737,80 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     int32_t* blc = barlist + c * g.nsb;
     double2* voc = vout + c * g.nsb;
 
-    // phase 1: thread-local pieces
+    CPG_CHAIN_MARK(T0)
+    // phase 1: thread-local pieces.  A thread owns `per` (<= kPre for chunks up to 1 Mi)
+    // consecutive blocks; their plans and composites are loaded up front, all in flight.
+    constexpr int kPre = 4;
+    const int cnt = (int)(b1 - b0);
+    const bool pre = cnt > 0 && cnt <= kPre;   // cnt == 0: the generic loops do nothing
+    // block b0 + i's plan and composites (i < cnt; callers unroll i)
+#define CPG_PREFETCH(P, A, B)                                  \
+    VitPlan P[kPre];                                           \
+    C64 A[kPre], B[kPre];                                      \
+    _Pragma("unroll") for (int i = 0; i < kPre; ++i) {         \
+        const int64_t kk = b0 + (i < cnt ? i : 0);             \
+        P[i] = pl[kk];                                         \
+        A[i] = ld_c64(cp + 2 * kk);                            \
+        B[i] = ld_c64(cp + 2 * kk + 1);                        \
+    }
     C64 run = c64_id(), lead = c64_id();
     bool hasb = false;
     int nb = 0;
-    for (int64_t k = b0; k < b1; ++k) {
-        const VitPlan p = pl[k];
+    auto piece = [&](int64_t k, const VitPlan& p, const C64& ca, const C64& cb) {
         if (p.type == PLAN_REGULAR) {
-            run = c64_mul(run, ld_c64(cp + 2 * k));
+            run = c64_mul(run, ca);
         } else {
-            if (p.type == PLAN_SPLIT) run = c64_mul(run, ld_c64(cp + 2 * k));
+            if (p.type == PLAN_SPLIT) run = c64_mul(run, ca);
             if (!hasb) lead = run;
             else st_c64(gkc + k, run);
             hasb = true;
             ++nb;
-            run = (p.type == PLAN_SPLIT) ? ld_c64(cp + 2 * k + 1) : c64_id();
+            run = (p.type == PLAN_SPLIT) ? cb : c64_id();
         }
+    };
+    if (pre) {
+        CPG_PREFETCH(xp, xa, xb)
+#pragma unroll
+        for (int i = 0; i < kPre; ++i)
+            if (i < cnt) piece(b0 + i, xp[i], xa[i], xb[i]);
+    } else {
+        for (int64_t k = b0; k < b1; ++k)
+            piece(k, pl[k], ld_c64(cp + 2 * k), ld_c64(cp + 2 * k + 1));
     }
     if (!hasb) lead = run;
-    // phase 2: segmented scan of (hasb, trail) + barrier count scan
-    __shared__ C64 sM[kChainT];
-    __shared__ int sF[kChainT];
-    __shared__ int sN[kChainT];
-    sM[t] = run;
-    sF[t] = hasb;
-    sN[t] = nb;
-    __syncthreads();
-    for (int off = 1; off < kChainT; off <<= 1) {
-        C64 m = sM[t];
-        int fl = sF[t], n = sN[t];
-        if (t >= off) {
-            if (!fl) m = c64_mul(sM[t - off], m);
-            fl |= sF[t - off];
-            n += sN[t - off];
-        }
-        __syncthreads();
-        sM[t] = m;
-        sF[t] = fl;
-        sN[t] = n;
-        __syncthreads();
+    CPG_CHAIN_MARK(T1)
+    // phase 2: segmented scan of (hasb, trail) + barrier count scan: shuffle scans inside
+    // each wave, then the 16 wave totals (exact max-plus products: any association)
+    struct Seg {
+        C64 m;
+        int fl, n;
+    };
+    auto seg_comb = [](const Seg& a, const Seg& b) {   // a before b
+        return Seg{b.fl ? b.m : c64_mul(a.m, b.m), a.fl | b.fl, a.n + b.n};
+    };
+    auto seg_shfl_up = [](const Seg& x, int d) {
+        return Seg{{__shfl_up(x.m.pp, d), __shfl_up(x.m.pm, d), __shfl_up(x.m.mp, d),
+                    __shfl_up(x.m.mm, d)},
+                   __shfl_up(x.fl, d), __shfl_up(x.n, d)};
+    };
+    const int lane = t & 63, wv = t >> 6;
+    Seg x{run, hasb ? 1 : 0, nb};
+#pragma unroll
+    for (int d = 1; d < 64; d <<= 1) {
+        const Seg y = seg_shfl_up(x, d);
+        if (lane >= d) x = seg_comb(y, x);
     }
-    const C64 incoming = t > 0 ? sM[t - 1] : c64_id();
-    const int bidx0 = t > 0 ? sN[t - 1] : 0;
-    const int nbar = sN[kChainT - 1];
+    __shared__ Seg sWave[kChainT / 64];
+    if (lane == 63) sWave[wv] = x;
+    __syncthreads();
+    Seg before{c64_id(), 0, 0};   // everything before this wave
+    for (int w = 0; w < wv; ++w) before = seg_comb(before, sWave[w]);
+    const Seg prev = seg_shfl_up(x, 1);   // inclusive value of the lane before
+    const Seg excl = lane > 0 ? seg_comb(before, prev) : before;
+    const C64 incoming = excl.m;
+    const int bidx0 = excl.n;
+    int nbar = 0;
+    for (int w = 0; w < kChainT / 64; ++w) nbar += sWave[w].n;
     {
         int idx = bidx0;
         bool first = true;
@@ -718,6 +826,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         }
     }
     __syncthreads();
+    CPG_CHAIN_MARK(T2)
     // phase 3: the serial chain over barriers.  The whole workgroup first stages every
     // window's step constants and every gap composite in LDS, so lane 0's serial
     // recurrence never waits on global memory; windows beyond the staging capacity fall
@@ -735,6 +844,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         sWk[t] = k;
         sWa[t] = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
         sWb[t] = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
+        if (k == 0) sWa[t] = sWb[t] = 0;   // block 0: walked by K1's head lanes
         sGap[t] = ld_c64(gpc + t);
     }
     __syncthreads();
@@ -759,10 +869,14 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         }
     }
     __syncthreads();
+    CPG_CHAIN_MARK(T3)
     if (t < 64) {
         double2 v = init;
         for (int i = 0; i < nbar; ++i) {
-            if (i < nst && sWoff[i] + max(0, sWb[i] - sWa[i]) <= kStageSteps) {
+            if (i == 0 && nst > 0 && sWk[0] == 0) {   // block 0 (always the first barrier)
+                v = vhead[c];
+                if (t == 0) voc[0] = v;
+            } else if (i < nst && sWoff[i] + max(0, sWb[i] - sWa[i]) <= kStageSteps) {
                 const C64 gp = sGap[i];
                 v = c64_apply(v, gp);
                 if (t == 0) {
@@ -789,28 +903,40 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
                 v = chain_window(pk, sL, stepL, k, ja, jb, v, t);
                 if (t == 0) voc[i] = v;
             }
-#ifdef CPG_DEBUG_CHAIN
-            if (t == 0 && c == 0)
-                printf("chain c0 barrier %d of %d staged %d\n", i, nbar, (int)(i < nst));
-#endif
         }
     }
     __syncthreads();
+    CPG_CHAIN_MARK(T4)
     // phase 4: entries
     double2 v = (bidx0 > 0) ? voc[bidx0 - 1] : init;
     if (t > 0) v = c64_apply(v, incoming);
     int idx = bidx0;
-    for (int64_t k = b0; k < b1; ++k) {
+    auto entries = [&](int64_t k, const VitPlan& p, const C64& ca, const C64& cb) {
         ent[k] = v;
-        const VitPlan p = pl[k];
         if (p.type == PLAN_REGULAR) {
-            v = c64_apply(v, ld_c64(cp + 2 * k));
+            v = c64_apply(v, ca);
         } else {
             v = voc[idx++];
-            if (p.type == PLAN_SPLIT) v = c64_apply(v, ld_c64(cp + 2 * k + 1));
+            if (p.type == PLAN_SPLIT) v = c64_apply(v, cb);
         }
+    };
+    if (pre) {
+        CPG_PREFETCH(xp, xa, xb)
+#pragma unroll
+        for (int i = 0; i < kPre; ++i)
+            if (i < cnt) entries(b0 + i, xp[i], xa[i], xb[i]);
+    } else {
+        for (int64_t k = b0; k < b1; ++k)
+            entries(k, pl[k], ld_c64(cp + 2 * k), ld_c64(cp + 2 * k + 1));
     }
     if (b1 == g.nsb && b0 < b1) ent[g.nsb] = v;
+    CPG_CHAIN_MARK(T5)
+#ifdef CPG_DEBUG_CHAIN
+    if (t == 0 && (c == 0 || c == g.nchunks - 1))
+        printf("chain c%lld nbar %d: phase1 %llu scan %llu list+stage %llu serial %llu entries %llu"
+               " (wall-clock ticks)\n", (long long)c, nbar, T1 - T0, T2 - T1, T3 - T2, T4 - T3,
+               T5 - T4);
+#endif
 }
 
 // ---------------------------------------------------------------- K5: re-forward
@@ -820,10 +946,16 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
                                                           uint4* __restrict__ bp,
                                                           uint8_t* __restrict__ origin,
                                                           uint32_t* status) {
-    __shared__ double2 LA[16], LB[16];   // conflict-free halves (256 B each)
+    // conflict-free halves (16 x 16 B each); entry 16 is the identity step (0, -inf, -inf,
+    // 0) standing for block 0's position 0: P + 0.0 = P and M + -inf = -inf exactly, so the
+    // values, the tie bits that matter and the origins are unchanged by it
+    __shared__ double2 LA[17], LB[17];
     if (threadIdx.x < 16) {
         LA[threadIdx.x] = make_double2(vc.L[threadIdx.x][0], vc.L[threadIdx.x][1]);
         LB[threadIdx.x] = make_double2(vc.L[threadIdx.x][2], vc.L[threadIdx.x][3]);
+    } else if (threadIdx.x == 16) {
+        LA[16] = make_double2(0.0, -INFINITY);
+        LB[16] = make_double2(-INFINITY, 0.0);
     }
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
@@ -862,7 +994,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
         const double2 la = LA[d], lb = LB[d];
         step2(la.x, la.y, lb.x, lb.y, q, jj);
     };
-    if (g.full(k)) {
+    if (g.whole(k)) {
         // quads of 64 steps; the ring of kLook lookups in flight runs across quad borders
         constexpr int kLook = 4;
         auto fetch = [&](uint32_t d) { return C64{LA[d].x, LA[d].y, LB[d].x, LB[d].y}; };
@@ -874,11 +1006,12 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
                           : ((ww[r] >> (2 * i - 2)) & 15u);
         };
         const int64_t wbase = k * kSBWords;
-        uint32_t prev = pk[wbase - 1];
+        uint32_t prev = k > 0 ? pk[wbase - 1] : 0u;
         uint4 cur = *reinterpret_cast<const uint4*>(pk + wbase);
         C64 ring[kLook];
 #pragma unroll
-        for (int j = 0; j < kLook; ++j) ring[j] = fetch(code(cur, prev, j));
+        for (int j = 0; j < kLook; ++j)
+            ring[j] = fetch((j == 0 && k == 0) ? 16u : code(cur, prev, j));
 #pragma unroll 1
         for (int q = 0; q < 4; ++q) {
             const uint4 nxt = *reinterpret_cast<const uint4*>(pk + wbase + 4 * (q < 3 ? q + 1 : q));
@@ -1024,6 +1157,7 @@ struct VitWs {
     double4* gap;
     int32_t* barlist;
     double2* vout;
+    double2* vhead;
     int32_t* splitlist;
     int32_t* splitcount;
     uint4* bp;
@@ -1053,6 +1187,7 @@ VitWs carve(void* base, int64_t nchunks, int64_t nsb) {
     w.gap = (double4*)take(nt * sizeof(double4));
     w.barlist = (int32_t*)take(nt * sizeof(int32_t));
     w.vout = (double2*)take(nt * sizeof(double2));
+    w.vhead = (double2*)take(nchunks * sizeof(double2));
     w.splitlist = (int32_t*)take(nt * sizeof(int32_t));
     w.splitcount = (int32_t*)take(nchunks * sizeof(int32_t));
     w.bp = (uint4*)take(nt * 4 * sizeof(uint4));
@@ -1082,20 +1217,19 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     const int64_t nt = nchunks * nsb;
     const unsigned grid = (unsigned)((nt + kThreads - 1) / kThreads);
     const size_t lds3 = (size_t)(vc.emax - vc.emin + 1) * 16 * sizeof(double4);
-    hipLaunchKernelGGL(k_vit_approx, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.comp1);
+    const unsigned head = (unsigned)((nchunks + kThreads - 1) / kThreads);
+    hipLaunchKernelGGL(k_vit_approx, dim3(grid + head), dim3(kThreads), 0, s, vc, packed, g,
+                       w.comp1, grid, w.vhead);
     hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks), dim3(kScanT), 0, s, vc, packed, g,
-                       w.comp1, w.aent, w.degen);
-    hipError_t me = hipMemsetAsync(w.splitcount, 0, nchunks * sizeof(int32_t), s);
-    if (me != hipSuccess) return me;
-    hipLaunchKernelGGL(k_vit_classify, dim3(grid), dim3(kThreads), 0, s, vc, g, w.aent, w.degen,
-                       w.plan, w.splitlist, w.splitcount);
+                       w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount);
     const size_t lds3x = (size_t)(vc.emax - vc.emin + 1) * (16 + 64) * 2 * sizeof(double2);
     hipLaunchKernelGGL(k_vit_exact, dim3(grid), dim3(kThreads), lds3x, s, vc, d_vt, packed, g,
                        w.plan, w.comp3, status);
     hipLaunchKernelGGL(k_vit_irregular, dim3((unsigned)nchunks), dim3(256), lds3, s, vc, d_vt,
                        packed, g, w.aent, w.plan, w.splitlist, w.splitcount, w.comp3);
     hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kChainT), 0, s, vc, packed, g,
-                       w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout);
+                       w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout,
+                       w.vhead);
     hipLaunchKernelGGL(k_vit_forward, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.degen,
                        w.entry, w.bp, w.origin, status);
     hipLaunchKernelGGL(k_vit_tscan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, g, w.entry,

@@ -14,7 +14,10 @@
  *   - every output buffer is caller-owned.  The context owns device workspace,
  *     pinned staging buffers and its stream.
  *   - one call at a time per context (contexts are internally serialised); separate
- *     contexts (one per device / process) run concurrently.
+ *     contexts (one per device / process) run concurrently.  Each kind of "_d" entry
+ *     point owns its own workspace in the context, so launches of DIFFERENT kinds (e.g.
+ *     the E-step and the Viterbi) may execute concurrently on different streams; two
+ *     launches of the same kind must be ordered by the caller (same stream or events).
  *   - "_d" entry points take DEVICE pointers (HBM-resident inputs, the bench path)
  *     and are asynchronous on `stream`; call cpg_sync() to wait and collect the
  *     context's device-side status word (set by the kernels' self checks).
@@ -149,7 +152,8 @@ int cpg_count_labelled_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t*
 
 /* Baum-Welch E-step (mapper) over whole chunk_len chunks; every chunk is an
  * independent observation sequence (:130-141).  d_counts: CPG_COUNTS_F64_N doubles
- * (cpg_counts_f64 layout), OVERWRITTEN.  Deterministic (fixed reduction order). */
+ * (cpg_counts_f64 layout), OVERWRITTEN.  Deterministic (fixed reduction order).
+ * chunk_len: a multiple of 4096, at most 65536 (the reference's 0x10000). */
 int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                    int64_t nbases, int64_t chunk_len, double* d_counts, void* stream);
 

@@ -30,7 +30,7 @@ if [[ $STEPS == *all* || $STEPS == *prof* ]]; then
   R=$(pwd)
   cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof -o run --output-format csv \
-      -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline > $R/$OUT/prof_bench.json 2> $R/$OUT/prof.err
+      -- python $R/bench.py --steps 5 --warmup 2 --no-cpu-baseline ${PROF_ARGS:---serial} > $R/$OUT/prof_bench.json 2> $R/$OUT/prof.err
   rc=$?; echo "rocprof rc=$rc"; cd $R
   find $OUT/prof -name "*stats*" | head; [ $rc -eq 0 ] || { tail -20 $OUT/prof.err; exit $rc; }
 fi
