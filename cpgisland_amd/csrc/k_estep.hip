@@ -43,7 +43,7 @@ constexpr int kSlab = 73;               // trans[64] (by dinucleotide x 4) | ini
 #endif
 constexpr int kRep = EST_REP;
 #ifndef EST_NREP
-#define EST_NREP 8
+#define EST_NREP 4
 #endif
 constexpr int kNRep = EST_NREP;   // bin replicas per wave (64 / kNRep lanes share one)
 // LDS: TA/TB (512 B) | union { 4-step tables, scan buffer, bins } | per-wave partials
@@ -72,14 +72,29 @@ __device__ __forceinline__ Mat mmul(const Mat& x, const Mat& y) {
     return r;
 }
 __device__ __forceinline__ Mat mid() { return {1.0, 0.0, 0.0, 1.0, 0}; }
+// product of two 2x2 matrices given as rows (x = row 0, y = row 1), not normalised
+__device__ __forceinline__ Mat mmul_raw(double2 xa, double2 xb, double2 ya, double2 yb) {
+    return {xa.x * ya.x + xa.y * yb.x, xa.x * ya.y + xa.y * yb.y, xb.x * ya.x + xb.y * yb.x,
+            xb.x * ya.y + xb.y * yb.y, 0};
+}
+__device__ __forceinline__ Mat shfl_up_mat(const Mat& x, int d) {
+    return {__shfl_up(x.a, d), __shfl_up(x.b, d), __shfl_up(x.c, d), __shfl_up(x.d, d),
+            __shfl_up(x.e, d)};
+}
+__device__ __forceinline__ Mat shfl_down_mat(const Mat& x, int d) {
+    return {__shfl_down(x.a, d), __shfl_down(x.b, d), __shfl_down(x.c, d), __shfl_down(x.d, d),
+            __shfl_down(x.e, d)};
+}
 
-__device__ __forceinline__ void vnorm(double& x, double& y) {
+__device__ __forceinline__ int vnorm(double& x, double& y) {   // returns the shift applied
     const double mx = fmax(x, y);
+    int k = 0;
     if (mx > 0.0) {
-        const int k = ilogb(mx);
+        k = ilogb(mx);
         x = ldexp(x, -k);
         y = ldexp(y, -k);
     }
+    return k;
 }
 
 // 1/z to full fp64 precision: hardware reciprocal + two Newton steps (explicit fma)
@@ -156,6 +171,11 @@ __device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int
     return c;
 }
 
+#ifdef CPG_DEBUG_ESTEP
+#define CPG_EST_MARK(n) const unsigned long long n = wall_clock64();
+#else
+#define CPG_EST_MARK(n)
+#endif
 __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
                                                      const uint32_t* __restrict__ packed,
                                                      int64_t C,
@@ -170,13 +190,15 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     // buffer (phase 2), the xi bins (phase 3) — each phase ends with a barrier
     double2* TA4 = TB + 16;                                   // 4-step products, row 0
     double2* TB4 = TA4 + 1024;                                //                  row 1
-    Mat* sm = reinterpret_cast<Mat*>(TA4);                    // [nl]
     auto* bins = reinterpret_cast<unsigned long long*>(TA4);  // [wave][kNRep][kRep]
     auto* part = reinterpret_cast<unsigned long long*>(
-        smem + kUnionOff + (kUnionBytes > nl * sizeof(Mat) ? kUnionBytes : nl * sizeof(Mat)));
+        smem + kUnionOff + kUnionBytes);
+    double4* fck4 = reinterpret_cast<double4*>(part + 16 * 64);   // [NMB-1][nl] products
+    double2* fck = reinterpret_cast<double2*>(fck4);              // then the checkpoints
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int64_t c = blockIdx.x;
+    CPG_EST_MARK(T0)
     const uint32_t* pk = packed + c * (C / 16);
     if (t < 16) {
         const int p = t & 3, b = t >> 2;
@@ -201,122 +223,152 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         TA4[i] = make_double2(x00, x01);
         TB4[i] = make_double2(x10, x11);
     }
-    const Codes cd = lane_codes(pk, t);
+    const Codes cd0 = lane_codes(pk, t);
     __syncthreads();
+    CPG_EST_MARK(T1)
 
     constexpr int L = kLanePos;            // 64 positions per lane
     constexpr int kMB = 16, NMB = L / kMB;
     const int p0 = t * L;
-    // 1. lane product of M_p over its positions, four matrices per lookup (position 0
-    //    carries no matrix: lane 0's first group is M_1 M_2 M_3)
+    // 1. lane product of M_p over its positions: per mini-block, its four 4-step matrices
+    //    multiplied as a tree (W0 W1)(W2 W3), then into the running product (position 0
+    //    carries no matrix: lane 0's first window is M_1 M_2 M_3).  The running products
+    //    after mini-blocks 0 .. NMB-2 (the alpha checkpoints' factors) go to LDS ([m][lane]
+    //    x 32 B; the exponent is dropped: alpha's scale per position is free).
     Mat P = mid();
-    Mat Pm[NMB - 1];   // products after mini-blocks 0 .. NMB-2: the alpha checkpoints
 #pragma unroll
-    for (int gq = 0; gq < L / 4; ++gq) {
-        double2 ra, rb;
-        if (t == 0 && gq == 0) {
-            double x00 = 1.0, x01 = 0.0, x10 = 0.0, x11 = 1.0;
-            const uint64_t cm = cd.mb(0);
+    for (int g = 0; g < NMB; ++g) {
+        double2 ra[4], rb[4];
 #pragma unroll
-            for (int i = 1; i < 4; ++i) {
-                const uint32_t d = code_at(cm, i);
-                const double2 ma = TA[d], mb = TB[d];
-                const double n00 = x00 * ma.x + x01 * mb.x, n01 = x00 * ma.y + x01 * mb.y;
-                const double n10 = x10 * ma.x + x11 * mb.x, n11 = x10 * ma.y + x11 * mb.y;
-                x00 = n00; x01 = n01; x10 = n10; x11 = n11;
+        for (int j = 0; j < 4; ++j) {
+            const int gq = 4 * g + j;
+            if (gq == 0 && t == 0) {
+                double x00 = 1.0, x01 = 0.0, x10 = 0.0, x11 = 1.0;
+                const uint64_t cm = cd0.mb(0);
+#pragma unroll
+                for (int i = 1; i < 4; ++i) {
+                    const uint32_t d = code_at(cm, i);
+                    const double2 ma = TA[d], mb = TB[d];
+                    const double n00 = x00 * ma.x + x01 * mb.x, n01 = x00 * ma.y + x01 * mb.y;
+                    const double n10 = x10 * ma.x + x11 * mb.x, n11 = x10 * ma.y + x11 * mb.y;
+                    x00 = n00; x01 = n01; x10 = n10; x11 = n11;
+                }
+                ra[j] = make_double2(x00, x01);
+                rb[j] = make_double2(x10, x11);
+            } else {
+                const uint32_t wi = cd0.win(gq);
+                ra[j] = TA4[wi];
+                rb[j] = TB4[wi];
             }
-            ra = make_double2(x00, x01);
-            rb = make_double2(x10, x11);
-        } else {
-            const uint32_t wi = cd.win(gq);
-            ra = TA4[wi];
-            rb = TB4[wi];
         }
-        Mat r{P.a * ra.x + P.b * rb.x, P.a * ra.y + P.b * rb.y, P.c * ra.x + P.d * rb.x,
-              P.c * ra.y + P.d * rb.y, P.e};
-        P = r;
-        if ((gq & 1) == 1) mnorm(P);
-        if ((gq & 3) == 3 && gq / 4 < NMB - 1) Pm[gq / 4] = P;
+        const Mat w01 = mmul_raw(ra[0], rb[0], ra[1], rb[1]);
+        const Mat w23 = mmul_raw(ra[2], rb[2], ra[3], rb[3]);
+        const Mat G{w01.a * w23.a + w01.b * w23.c, w01.a * w23.b + w01.b * w23.d,
+                    w01.c * w23.a + w01.d * w23.c, w01.c * w23.b + w01.d * w23.d, 0};
+        P = mmul(P, G);   // normalised
+        if (g < NMB - 1) fck4[g * nl + t] = make_double4(P.a, P.b, P.c, P.d);
     }
-    __syncthreads();   // the 4-step tables are dead from here: the scan buffer reuses them
-    // 2a. inclusive prefix (Hillis-Steele)
-    sm[t] = P;
+    CPG_EST_MARK(T2)
+    // 2. prefix and suffix products of the lane products: shuffle scans inside each wave
+    //    (interleaved), one wave scans the wave totals, two barriers in all
+    const int wv = t >> 6;
+    Mat xp = P, xs = P;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const Mat yp = shfl_up_mat(xp, off), ys = shfl_down_mat(xs, off);
+        if (lane >= off) xp = mmul(yp, xp);
+        if (lane + off < 64) xs = mmul(xs, ys);
+    }
+    const Mat up1 = shfl_up_mat(xp, 1), dn1 = shfl_down_mat(xs, 1);
+    __syncthreads();   // every lane is past its 4-step table reads: the union is free
+    Mat* sWP = reinterpret_cast<Mat*>(TA4);   // [16] wave products (prefix order)
+    Mat* sWS = sWP + 16;                      // [16] wave products (suffix order)
+    Mat* sXP = sWS + 16;                      // [17] products of the waves before; [16] all
+    Mat* sXS = sXP + 17;                      // [16] products of the waves after
+    if (lane == 63) sWP[wv] = xp;
+    if (lane == 0) sWS[wv] = xs;
     __syncthreads();
-    for (int off = 1; off < nl; off <<= 1) {
-        Mat x = sm[t];
-        if (t >= off) x = mmul(sm[t - off], x);
-        __syncthreads();
-        sm[t] = x;
-        __syncthreads();
+    if (t < 64) {
+        Mat wp = t < nw ? sWP[t] : mid(), ws = t < nw ? sWS[t] : mid();
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const Mat yp = shfl_up_mat(wp, off), ys = shfl_down_mat(ws, off);
+            if (t >= off) wp = mmul(yp, wp);
+            if (t + off < 16) ws = mmul(ws, ys);
+        }
+        const Mat ep = shfl_up_mat(wp, 1), es = shfl_down_mat(ws, 1);
+        if (t < nw) {
+            sXP[t] = t > 0 ? ep : mid();
+            sXS[t] = t + 1 < nw ? es : mid();
+        }
+        if (t == nw - 1) sXP[16] = wp;
     }
+    __syncthreads();
     const uint32_t o0 = pk[0] & 3u;
     const double fa = model.pi[o0], fb = model.pi[o0 + 4];   // alpha_0 (b = 1 when live)
     double loglik = 0.0;
     if (t == nl - 1) {
-        const Mat A = sm[nl - 1];
+        const Mat A = sXP[16];
         loglik = log(fa * (A.a + A.b) + fb * (A.c + A.d)) + (double)A.e * 0.69314718055994530942;
     }
-    double aP, aM;   // alpha at position p0-1 (t > 0); alpha_0 for t == 0
+    double aP = fa, aM = fb;   // alpha at position p0-1 (t > 0); alpha_0 for t == 0
     if (t > 0) {
-        const Mat A = sm[t - 1];
+        const Mat A = lane > 0 ? mmul(sXP[wv], up1) : sXP[wv];
         aP = fa * A.a + fb * A.c;
         aM = fa * A.b + fb * A.d;
-    } else {
-        aP = fa;
-        aM = fb;
     }
     vnorm(aP, aM);
-    double fcP[NMB], fcM[NMB];   // the alpha checkpoints (see 3a)
-    fcP[0] = aP;
-    fcM[0] = aM;
-#pragma unroll
-    for (int m = 1; m < NMB; ++m) {
-        const Mat& A = Pm[m - 1];
-        fcP[m] = aP * A.a + aM * A.c;
-        fcM[m] = aP * A.b + aM * A.d;
-        vnorm(fcP[m], fcM[m]);
-    }
-    __syncthreads();
-    // 2b. inclusive suffix
-    sm[t] = P;
-    __syncthreads();
-    for (int off = 1; off < nl; off <<= 1) {
-        Mat x = sm[t];
-        if (t + off < nl) x = mmul(x, sm[t + off]);
-        __syncthreads();
-        sm[t] = x;
-        __syncthreads();
-    }
     double bP = 1.0, bM = 1.0;   // beta at the lane's last position
     if (t + 1 < nl) {
-        const Mat B = sm[t + 1];
+        const Mat B = lane < 63 ? mmul(dn1, sXS[wv]) : sXS[wv];
         bP = B.a + B.b;
         bM = B.c + B.d;
     }
     vnorm(bP, bM);
+    CPG_EST_MARK(T3)
+    // the alpha checkpoints (see 3a) of mini-blocks 1.. in LDS ([m-1][lane], 16-B rows:
+    // conflict-free), mini-block 0's is (aP, aM) itself: registers stay below 128
+#pragma unroll
+    for (int m = 1; m < NMB; ++m) {
+        const double4 A = fck4[(m - 1) * nl + t];
+        double xP = aP * A.x + aM * A.z, xM = aP * A.y + aM * A.w;
+        vnorm(xP, xM);
+        fck[2 * ((m - 1) * nl + t)] = make_double2(xP, xM);
+    }
     __syncthreads();
+    CPG_EST_MARK(T4)
 
     // 3a. bins (aliasing the scan buffer, read above) zeroed; alpha entering mini-block m
     //     = alpha entering the lane times phase 1's product of the first m mini-blocks
     //     (any per-position scale cancels in the normalised xi)
     for (int i = t; i < nw * kNRep * kRep; i += nl) bins[i] = 0ull;
     __syncthreads();
+    CPG_EST_MARK(T5)
+    const Codes cd = lane_codes(pk, t);   // 20 B from L2 again rather than 13 live VGPRs
     // 3b. mini-blocks, last to first: forward alphas in registers from the checkpoint, then
     //     backward with xi accumulation; beta flows on from one mini-block to the previous
     unsigned long long* wb = bins + ((t >> 6) * kNRep + lane / (64 / kNRep)) * kRep;
     double g0P = 0.0, g0M = 0.0;
     double yP = bP, yM = bM;   // beta at the last position of the mini-block
-#pragma unroll 1
+#ifndef EST_ABL
+#define EST_ABL 0
+#endif
+    unsigned long long sink = 0;   // ablations only
+#ifndef EST_MB_UNROLL
+#define EST_MB_UNROLL 1
+#endif
+#pragma unroll EST_MB_UNROLL
     for (int m = NMB - 1; m >= 0; --m) {
-        const uint64_t cm = cd.mb(m);
+        const uint64_t cm = cd.mb(m);   // (codes re-derived after the scans: see 3a)
         // alpha at the position before the mini-block (select chain: no register indexing)
-        double bfP = fcP[0], bfM = fcM[0];
-#pragma unroll
-        for (int k = 1; k < NMB; ++k) {
-            bfP = m == k ? fcP[k] : bfP;
-            bfM = m == k ? fcM[k] : bfM;
+        double bfP = aP, bfM = aM;
+        if (m > 0) {
+            const double2 f = fck[2 * ((m - 1) * nl + t)];
+            bfP = f.x;
+            bfM = f.y;
         }
         double alP[kMB], alM[kMB];
+        int kf[kMB / 4];   // alpha's power-of-two shifts after positions 3, 7, 11
         double xP = bfP, xM = bfM;
 #pragma unroll
         for (int i = 0; i < kMB; ++i) {
@@ -330,10 +382,16 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
             xP = nP;
             xM = nM;
-            if ((i & 3) == 3) vnorm(xP, xM);
+            if ((i & 3) == 3) kf[i >> 2] = vnorm(xP, xM);
             alP[i] = xP;
             alM[i] = xM;
         }
+        // Z_p = alpha_{p-1}^T M_p beta_p is the same at every position up to the exact
+        // power-of-two rescalings of alpha and beta, so one reciprocal per mini-block (at its
+        // last position) normalises every xi: rz_p = rz_15 * 2^(eb - ef), eb = beta's shifts
+        // since position 15, ef = alpha's shifts between positions p-1 and 14
+        double rz0 = 0.0, rz = 0.0;
+        int eb = 0, ef = 0;
 #pragma unroll
         for (int i = kMB - 1; i >= 0; --i) {
             if (t == 0 && m == 0 && i == 0) {   // gamma_0 -> init counts
@@ -345,21 +403,45 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             const double uP = i > 0 ? alP[i - 1] : bfP;
             const double uM = i > 0 ? alM[i - 1] : bfM;
             const uint32_t d = code_at(cm, i);
+#if EST_ABL == 3   // development ablation: no table reads in the backward pass
+            const double2 ma = make_double2(0.5 + d * 1e-3, 0.25), mb = make_double2(0.125, 0.5);
+#else
             const double2 ma = TA[d], mb = TB[d];
-            const double x00 = uP * ma.x * yP, x01 = uP * ma.y * yM, x10 = uM * mb.x * yP,
-                         x11 = uM * mb.y * yM;
-            const double rz = rcp_nr((x00 + x01) + (x10 + x11)) * kFix;   // exact scaling
+#endif
+            // M beta products, shared by the pair marginals and the beta update
+            const double t00 = ma.x * yP, t01 = ma.y * yM, t10 = mb.x * yP, t11 = mb.y * yM;
+            const double x00 = uP * t00, x01 = uP * t01, x10 = uM * t10, x11 = uM * t11;
+            if (i == kMB - 1) {
+                rz0 = rcp_nr((x00 + x01) + (x10 + x11)) * kFix;
+                rz = rz0;
+            } else if ((i & 3) == 3) {
+                ef += kf[i >> 2];
+                rz = ldexp(rz0, eb - ef);
+            }
+#if EST_ABL == 1   // development ablation: no LDS atomics (wrong results, timing only)
+            sink += to_fixed_scaled(x00 * rz) ^ to_fixed_scaled(x01 * rz) ^
+                    to_fixed_scaled(x10 * rz) ^ to_fixed_scaled(x11 * rz) ^ d;
+#elif EST_ABL == 2   // development ablation: collision-free lane-private bins
+            {
+                unsigned long long* pb = bins + ((t & 1023) % (nw * kNRep * kRep / 4)) * 4;
+                atomicAdd(pb + 0, to_fixed_scaled(x00 * rz));
+                atomicAdd(pb + 1, to_fixed_scaled(x01 * rz));
+                atomicAdd(pb + 2, to_fixed_scaled(x10 * rz));
+                atomicAdd(pb + 3, to_fixed_scaled(x11 * rz) + d);
+            }
+#else
             atomicAdd(wb + bin_of(d, 0), to_fixed_scaled(x00 * rz));
             atomicAdd(wb + bin_of(d, 1), to_fixed_scaled(x01 * rz));
             atomicAdd(wb + bin_of(d, 2), to_fixed_scaled(x10 * rz));
             atomicAdd(wb + bin_of(d, 3), to_fixed_scaled(x11 * rz));
-            const double nP = ma.x * yP + ma.y * yM, nM = mb.x * yP + mb.y * yM;
-            yP = nP;
-            yM = nM;
-            if ((i & 3) == 0) vnorm(yP, yM);
+#endif
+            yP = t00 + t01;
+            yM = t10 + t11;
+            if ((i & 3) == 0) eb += vnorm(yP, yM);
         }
     }
     __syncthreads();
+    CPG_EST_MARK(T6)
     // chunk totals of the nw * kNRep replicas: wave q sums replicas q, q + nw, ... of every
     // bin (integer sums: exact in any order), then 64 lanes add the nw partials
     {
@@ -369,6 +451,7 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         part[q * 64 + lane] = s;
     }
     __syncthreads();
+    CPG_EST_MARK(T7)
     // chunk results -> the global 128-bit accumulators: xi bins and the init posteriors in
     // 2^-47 units, the log-likelihood in signed 2^-24 units
     if (t < 64) {   // row t = d * 4 + k
@@ -376,6 +459,7 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         for (int q = 0; q < nw; ++q) s += part[q * 64 + t];
         acc128_add(acc + 2 * t, s, false);
     }
+    if (EST_ABL && sink == 0x123456789ull) acc[0] = sink;   // keep the ablated work live
     if (t == 0) {
         acc128_add(acc + 2 * (64 + o0), to_fixed_scaled(g0P * kFix), false);
         acc128_add(acc + 2 * (64 + o0 + 4), to_fixed_scaled(g0M * kFix), false);
@@ -384,6 +468,12 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         const long long L = llrint(ldexp(loglik, kLogFix));
         acc128_add(acc + 2 * 72, (unsigned long long)L, L < 0);
     }
+#ifdef CPG_DEBUG_ESTEP
+    if (t == 0 && (c == 0 || c == 300 || c == (int64_t)gridDim.x - 1))
+        printf("estep c%lld: tables %llu product %llu scans %llu ckpt %llu zero %llu main %llu "
+               "binsum %llu (wall-clock ticks, 100 MHz)\n", (long long)c, T1 - T0, T2 - T1,
+               T3 - T2, T4 - T3, T5 - T4, T6 - T5, T7 - T6);
+#endif
 }
 
 __device__ void final_estep(const double* v, int t, double* __restrict__ out);
@@ -442,9 +532,9 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
     if (C % 4096 || C > (int64_t)kET * kLanePos) return hipErrorInvalidValue;
     if (nchunks == 0) return hipMemsetAsync(out, 0, 105 * sizeof(double), s);
     const int lanes = (int)(C / kLanePos);
-    // the union is sized for 16 waves; a smaller chunk (fewer lanes) uses a prefix of it
-    const size_t uni = std::max(kUnionBytes, (size_t)lanes * sizeof(Mat));
-    const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long);
+    const size_t uni = kUnionBytes;   // sized for 16 waves; fewer lanes use a prefix
+    const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long) +
+                       (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
     hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
                        packed, C, acc);
     hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);
