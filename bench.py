@@ -40,6 +40,23 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def _pmc_traffic(kernel, nbases):
+    """HBM bytes per launch of `kernel` from the committed PMC summary of this bench
+    (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction of
+    MI355X_MICROARCH.md), when it was collected on the same workload size."""
+    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+    try:
+        with open(path) as f:
+            d = json.load(f)
+        k = d["kernels"][kernel]
+        if d.get("bases") != nbases:
+            return None
+        return {"traffic_bytes": int(k["traffic_bytes"]),
+                "source": f"profiles/pmc_latest.json ({d.get('collected', '?')})"}
+    except (OSError, KeyError, ValueError):
+        return None
+
+
 def cpu_baseline(seed, sample_bases):
     """The oracle (C restatement of the reference, Mahout-order 8-state Viterbi with
     Math.log in the inner loop, textbook E-step, counts, island scan) on 1 host core over a
@@ -71,6 +88,8 @@ def main():
     ap.add_argument("--bases", type=int, default=N_PER_GPU, help="bases per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-sample", type=int, default=8 * DECODE)
+    ap.add_argument("--prio", type=int, default=1,
+                    help="1: decode stream at high priority (two-stream mode)")
     ap.add_argument("--serial", action="store_true",
                     help="train and decode phases on one stream (isolated phase timing)")
     ap.add_argument("--flush-mb", type=int, default=0,
@@ -133,7 +152,9 @@ def main():
     # that the E-step fills).  --serial runs everything on one stream (isolated phase times).
     main_s = torch.cuda.current_stream()
     s_tr = main_s if args.serial else torch.cuda.Stream()
-    s_dec = main_s if args.serial else torch.cuda.Stream()
+    # the decode stream at high priority: its latency-bound kernels get CUs first as the
+    # E-step's workgroups retire, the E-step fills the rest
+    s_dec = main_s if args.serial else torch.cuda.Stream(priority=-1 if args.prio else 0)
 
     def step(it):
         def mark(k, i):
@@ -201,13 +222,27 @@ def main():
         value = N * world / (phases_total / 1e3)
 
     if rank == 0:
-        dom = max(("estep", "counts", "viterbi", "islands"), key=lambda k: phases[k])
-        ach = BYTES_PER_BASE[dom] * N / (phases[dom] / 1e3) / 1e9
-        roof = {"bound": "hbm", "kernel": dom, "achieved": round(ach, 1), "peak": HBM_PEAK_GBS,
-                "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "bytes_per_base": BYTES_PER_BASE[dom],
-                "note": "phase time from HIP events on the launch stream; see DESIGN.md for "
-                        "the VALU bound of the fp64 phases"}
+        # dominant kernel (rocprof, profiles/): the E-step chunk kernel.  achieved = its
+        # algorithmic bytes per launch / the phase's mean duration (HIP events on its stream;
+        # the phase is k_estep_chunk + the ~4 us one-workgroup final kernel).
+        dom = "estep"
+        alg_bytes = BYTES_PER_BASE[dom] * N
+        ach = alg_bytes / (phases[dom] / 1e3) / 1e9
+        roof = {"bound": "hbm", "kernel": "k_estep_chunk", "phase": dom,
+                "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                "algorithmic_bytes": alg_bytes, "bytes_per_base": BYTES_PER_BASE[dom]}
+        pmc = _pmc_traffic("k_estep_chunk", N)
+        if pmc:
+            roof["traffic"] = pmc["traffic_bytes"]
+            roof["traffic_source"] = pmc["source"]
+        roof["note"] = ("not HBM-bound: LDS/VALU/latency-bound fp64 forward-backward "
+                        "(DESIGN.md 5, profiles/*pmc*)")
+        vit = phases["viterbi"] + phases["islands"]
+        roof_decode = {"phase": "viterbi+islands", "achieved": round(
+            (BYTES_PER_BASE["viterbi"] + BYTES_PER_BASE["islands"]) * N / (vit / 1e3) / 1e9, 1),
+            "unit": "GB/s", "frac": None}
+        roof_decode["frac"] = round(roof_decode["achieved"] / HBM_PEAK_GBS, 4)
         out = {"metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
                "steps": steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
@@ -216,11 +251,12 @@ def main():
                "config": {"workload": "C2: 46 Mbp chr21-sized per GPU; BW E-step + labelled "
                                       "counts + RCCL reduce + exact Viterbi + islands",
                           "streams": 1 if args.serial else 2,
+                          "decode_priority": "high" if (args.prio and not args.serial) else "normal",
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
                           "islands_found": int(icnt.item())},
                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
-               "roofline": roof}
+               "roofline": roof, "roofline_decode": roof_decode}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(SEED, args.cpu_sample)
         else:

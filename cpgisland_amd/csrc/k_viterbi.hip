@@ -81,6 +81,9 @@ __device__ __forceinline__ CI ci_mul(const CI& a, const CI& b) {
     return {cl(mx(a.pp + b.pp, a.pm + b.mp)), cl(mx(a.pp + b.pm, a.pm + b.mm)),
             cl(mx(a.mp + b.pp, a.mm + b.mp)), cl(mx(a.mp + b.pm, a.mm + b.mm))};
 }
+__device__ __forceinline__ CI shfl_up_ci(const CI& x, int d) {
+    return {__shfl_up(x.pp, d), __shfl_up(x.pm, d), __shfl_up(x.mp, d), __shfl_up(x.mm, d)};
+}
 __device__ __forceinline__ void ci_apply(int64_t& P, int64_t& M, const CI& c) {
     int64_t nP = cl(mx(P + c.pp, M + c.mp)), nM = cl(mx(P + c.pm, M + c.mm));
     P = nP;
@@ -379,7 +382,7 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
     const int4* cc = comp + c * g.nsb;
     longlong2* ae = aent + c * (g.nsb + 1);
     VitPlan* pl = plan + c * g.nsb;
-    __shared__ CI buf[kScanT];
+    __shared__ CI buf[kScanT / 64];   // wave products
     __shared__ int sIrr;
     const int64_t per = (g.nsb + kScanT - 1) / kScanT;
     const int64_t b0 = min((int64_t)t * per, g.nsb), b1 = min(b0 + per, g.nsb);
@@ -400,18 +403,23 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
         const int4 x = cc[k];
         prod = ci_mul(prod, CI{x.x, x.y, x.z, x.w});
     }
-    buf[t] = prod;
-    __syncthreads();
-    for (int off = 1; off < kScanT; off <<= 1) {
-        CI v = buf[t];
-        if (t >= off) v = ci_mul(buf[t - off], v);
-        __syncthreads();
-        buf[t] = v;
-        __syncthreads();
+    // exclusive scan of the lanes' products: shuffles inside each wave, then the wave totals
+    const int lane = t & 63, wv = t >> 6;
+    CI x = prod;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const CI y = shfl_up_ci(x, off);
+        if (lane >= off) x = ci_mul(y, x);
     }
+    const CI up1 = shfl_up_ci(x, 1);
+    if (lane == 63) buf[wv] = x;
+    __syncthreads();
+    CI excl = ci_id();
+    for (int w = 0; w < wv; ++w) excl = ci_mul(excl, buf[w]);
+    if (lane > 0) excl = ci_mul(excl, up1);
     const int f = vc.qshift;
     int64_t P = fix_of(lp, f), M = fix_of(lm, f);
-    if (t > 0) ci_apply(P, M, buf[t - 1]);
+    if (t > 0) ci_apply(P, M, excl);
     for (int64_t k = b0; k < b1; ++k) {
         const longlong2 en = make_longlong2(P, M);
         ae[k] = en;
@@ -437,11 +445,21 @@ __device__ __forceinline__ bool c64_exact(const C64& c, int e, double spread) {
     return c64_absmax(c) + spread < ldexp(1.0, e + 1);
 }
 
+__device__ void vit_irregular(const VitConsts& vc, const uint32_t* packed, const Geo& g,
+                              const longlong2* __restrict__ aent, VitPlan* __restrict__ plan,
+                              const int32_t* __restrict__ irrlist,
+                              const int32_t* __restrict__ irrcount,
+                              double4* __restrict__ comp3, int64_t c, const double2* sA,
+                              const double2* sB);
+
 __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitTables* vt,
                                                         const uint32_t* packed, Geo g,
                                                         VitPlan* __restrict__ plan,
                                                         double4* __restrict__ comp3,
-                                                        uint32_t* status) {
+                                                        uint32_t* status, unsigned main_grid,
+                                                        const longlong2* __restrict__ aent,
+                                                        const int32_t* __restrict__ irrlist,
+                                                        const int32_t* __restrict__ irrcount) {
     // per binade slot: single-step halves sA/sB [16] (one 256-B bank row each) and 2-step
     // composites over 3-base windows, halves P2A = (pp, pm), P2B = (mp, mm) [64].  Every
     // entry is a sum of binade-rounded constants: exact on the binade's grid.
@@ -467,6 +485,11 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
         P2B[i] = make_double2(m.mp, m.mm);
     }
     __syncthreads();
+    if (blockIdx.x >= main_grid) {   // workgroup-uniform: the chunk's irregular blocks
+        vit_irregular(vc, packed, g, aent, plan, irrlist, irrcount, comp3,
+                      (int64_t)(blockIdx.x - main_grid), sA, sB);
+        return;
+    }
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;
     const VitPlan p = plan[gid];
@@ -534,26 +557,18 @@ __device__ __forceinline__ void walk_piece(const uint32_t* __restrict__ pk, int6
     }
 }
 
-__global__ __launch_bounds__(256) void k_vit_irregular(VitConsts vc, const VitTables* vt,
-                                                      const uint32_t* packed, Geo g,
-                                                      const longlong2* __restrict__ aent,
-                                                      VitPlan* __restrict__ plan,
-                                                      const int32_t* __restrict__ irrlist,
-                                                      const int32_t* __restrict__ irrcount,
-                                                      double4* __restrict__ comp3) {
-    extern __shared__ __attribute__((aligned(16))) double2 sLe[];   // [A|B][e - emin][16]
+// Runs in K3's launch as one extra workgroup per chunk (concurrently with the regular
+// blocks' composites); sA/sB: K3's single-step binade tables [e - emin][16]
+__device__ void vit_irregular(const VitConsts& vc, const uint32_t* packed, const Geo& g,
+                              const longlong2* __restrict__ aent, VitPlan* __restrict__ plan,
+                              const int32_t* __restrict__ irrlist,
+                              const int32_t* __restrict__ irrcount,
+                              double4* __restrict__ comp3, int64_t c, const double2* sA,
+                              const double2* sB) {
     __shared__ int4 Q[16];
-    const int64_t c = blockIdx.x;
     const int n = irrcount[c];
-    if (n == 0) return;
+    if (n == 0) return;   // workgroup-uniform
     const int nb = vc.emax - vc.emin + 1;
-    double2* sA = sLe;
-    double2* sB = sLe + nb * 16;
-    for (int i = threadIdx.x; i < nb * 16; i += 256) {
-        const double* s = vt->Le[vc.emin + i / 16][i % 16];
-        sA[i] = make_double2(s[0], s[1]);
-        sB[i] = make_double2(s[2], s[3]);
-    }
     if (threadIdx.x < 16)
         Q[threadIdx.x] = make_int4(vc.Q[threadIdx.x][0], vc.Q[threadIdx.x][1],
                                    vc.Q[threadIdx.x][2], vc.Q[threadIdx.x][3]);
@@ -1216,17 +1231,16 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     Geo g{nchunks, chunk_len, nsb};
     const int64_t nt = nchunks * nsb;
     const unsigned grid = (unsigned)((nt + kThreads - 1) / kThreads);
-    const size_t lds3 = (size_t)(vc.emax - vc.emin + 1) * 16 * sizeof(double4);
     const unsigned head = (unsigned)((nchunks + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(k_vit_approx, dim3(grid + head), dim3(kThreads), 0, s, vc, packed, g,
                        w.comp1, grid, w.vhead);
     hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks), dim3(kScanT), 0, s, vc, packed, g,
                        w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount);
     const size_t lds3x = (size_t)(vc.emax - vc.emin + 1) * (16 + 64) * 2 * sizeof(double2);
-    hipLaunchKernelGGL(k_vit_exact, dim3(grid), dim3(kThreads), lds3x, s, vc, d_vt, packed, g,
-                       w.plan, w.comp3, status);
-    hipLaunchKernelGGL(k_vit_irregular, dim3((unsigned)nchunks), dim3(256), lds3, s, vc, d_vt,
-                       packed, g, w.aent, w.plan, w.splitlist, w.splitcount, w.comp3);
+    // K3 + K3b in one launch: the chunks' irregular blocks run as extra workgroups
+    hipLaunchKernelGGL(k_vit_exact, dim3(grid + (unsigned)nchunks), dim3(kThreads), lds3x, s, vc,
+                       d_vt, packed, g, w.plan, w.comp3, status, grid, w.aent, w.splitlist,
+                       w.splitcount);
     hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kChainT), 0, s, vc, packed, g,
                        w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout,
                        w.vhead);

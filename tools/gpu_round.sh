@@ -34,4 +34,7 @@ if [[ $STEPS == *all* || $STEPS == *prof* ]]; then
   rc=$?; echo "rocprof rc=$rc"; cd $R
   find $OUT/prof -name "*stats*" | head; [ $rc -eq 0 ] || { tail -20 $OUT/prof.err; exit $rc; }
 fi
+if [[ $STEPS == *pmc* ]]; then
+  bash tools/pmc.sh; rc=$?; echo "pmc rc=$rc"; [ $rc -eq 0 ] || exit $rc
+fi
 echo done

@@ -49,4 +49,7 @@ for k in sorted(vals, key=lambda k: -sum(dur.get(k, [0]))):
     out[k] = {"dur_us": d, "fetch_bytes": fetch, "write_bytes": write,
               "traffic_bytes": fetch + write, **{c: v[c] for c in v}}
 if len(sys.argv) > 2:
-    json.dump(out, open(sys.argv[2], "w"), indent=1, sort_keys=True)
+    import time
+    json.dump({"bases": int(sys.argv[3]) if len(sys.argv) > 3 else None,
+               "collected": time.strftime("%Y-%m-%d") + " tools/pmc.sh (bench.py --serial)",
+               "kernels": out}, open(sys.argv[2], "w"), indent=1, sort_keys=True)
