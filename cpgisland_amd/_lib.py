@@ -74,6 +74,8 @@ SIGNATURES = {
     "cpg_viterbi": [_P, _P, _P, _I64, _I64, _P, _P],
     "cpg_decode_states": [_P, _P, _P, _I64, _P],
     "cpg_islands": [_P, _P, _P, _I64, _I64, _P, _I64, _P],
+    "cpg_ingest_d": [_P, _P, _I64, _INT, _INT, _P, _I64, _P, _P],
+    "cpg_ingest_gpu": [_P, C.c_char_p, C.c_size_t, _INT, _INT, _P, _I64, _P],
 }
 
 

@@ -50,7 +50,7 @@ int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
 namespace {
 
 enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
-       WS_OUT1 = 7, WS_OUT2 = 8 };
+       WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9 };
 
 // NULL is the HIP null stream (torch's default stream handle is 0 too); the host-buffer
 // wrappers pass the context's own stream explicitly
@@ -268,6 +268,27 @@ int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packe
     return CPG_OK;
 }
 
+int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compat_quirks,
+                 uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result,
+                 void* stream) {
+    if (!ctx || !d_result || (n > 0 && !d_txt) || (cap_bases > 0 && !d_packed))
+        return set_error(CPG_E_INVALID, "cpg_ingest_d: null argument");
+    if (n < 0 || cap_bases < 0 || (mode != 0 && mode != 1))
+        return set_error(CPG_E_INVALID, "cpg_ingest_d: bad argument");
+    if (!aligned16(d_txt) || !aligned16(d_packed))
+        return set_error(CPG_E_INVALID, "cpg_ingest_d: buffers must be 16-byte aligned");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    void* ws;
+    int rc;
+    if ((rc = ws_get(ctx, WS_ING, ingest_ws_bytes(n), &ws))) return rc;
+    CPG_HIP(launch_ingest(reinterpret_cast<const uint8_t*>(d_txt), n, mode, compat_quirks,
+                          mode == 0 ? CPG_TRAIN_CHUNK : CPG_DECODE_CHUNK, d_packed, cap_bases,
+                          ws, ctx->ws[WS_ING].bytes, reinterpret_cast<long long*>(d_result),
+                          pick(ctx, stream)));
+    return CPG_OK;
+}
+
 // ---- host-buffer entry points -------------------------------------------------------
 #define CPG_TRY(x)              \
     do {                        \
@@ -362,6 +383,42 @@ int cpg_decode_states(cpg_ctx* ctx, const cpg_model* model, const int32_t* obs, 
         states_out[i] = obs[i] + (plus ? 0 : 4);
         if (degen && (i < n - 1 || n == 1)) states_out[i] = 0;
     }
+    return CPG_OK;
+}
+
+int cpg_ingest_gpu(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat_quirks,
+                   uint32_t* packed, int64_t cap_bases, int64_t* nbases) {
+    if (!ctx || !nbases || (n > 0 && !txt) || (cap_bases > 0 && !packed) || cap_bases < 0 ||
+        (mode != 0 && mode != 1))
+        return set_error(CPG_E_INVALID, "cpg_ingest_gpu: bad argument");
+    *nbases = 0;
+    void *dt, *dp, *dr;
+    {
+        std::lock_guard<std::mutex> lk(ctx->mu);
+        CPG_HIP(hipSetDevice(ctx->device));
+        CPG_TRY(stage_in(ctx, WS_IN0, txt, n, &dt));
+        CPG_TRY(ws_get(ctx, WS_OUT0, (size_t)((cap_bases + 15) / 16) * 4 + 16, &dp));
+        CPG_TRY(ws_get(ctx, WS_OUT1, sizeof(cpg_ingest_result), &dr));
+    }
+    CPG_TRY(cpg_ingest_d(ctx, (const char*)dt, (int64_t)n, mode, compat_quirks, (uint32_t*)dp,
+                         cap_bases, (cpg_ingest_result*)dr, ctx->stream));
+    cpg_ingest_result r;
+    CPG_HIP(hipMemcpyAsync(&r, dr, sizeof r, hipMemcpyDeviceToHost, ctx->stream));
+    CPG_TRY(cpg_sync(ctx, ctx->stream));
+    *nbases = r.nbases;
+    // the committed chunks (and, as cpg_ingest, the pending tail bases that fit)
+    const int64_t keep = r.status == CPG_OK ? cap_bases : r.nbases;
+    if (keep > 0)
+        CPG_HIP(hipMemcpy(packed, dp, (size_t)((keep + 15) / 16) * 4, hipMemcpyDeviceToHost));
+    if (r.status == CPG_E_REF_CRASH)
+        return set_error(CPG_E_REF_CRASH,
+                         "reference throws at input byte %lld (decode reader on an empty list, "
+                         "or the base count wrapped past 2^32)", (long long)r.crash_byte);
+    if (r.status == CPG_E_CAPACITY)
+        return set_error(CPG_E_CAPACITY, "cpg_ingest_gpu: capacity %lld bases exceeded",
+                         (long long)cap_bases);
+    if (r.status != CPG_OK)
+        return set_error((int)r.status, "cpg_ingest_gpu: device look-back timed out");
     return CPG_OK;
 }
 

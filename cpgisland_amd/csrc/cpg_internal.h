@@ -111,4 +111,9 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
                         hipStream_t s);
 size_t estep_ws_bytes(int64_t nchunks, int64_t chunk_len);
 
+hipError_t launch_ingest(const uint8_t* txt, int64_t n, int mode, int quirks, int64_t chunk,
+                         uint32_t* out, int64_t cap, void* ws, size_t ws_bytes,
+                         long long* res, hipStream_t s);
+size_t ingest_ws_bytes(int64_t n);
+
 }  // namespace cpg

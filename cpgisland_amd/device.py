@@ -102,3 +102,32 @@ def sign_to_numpy(sign: torch.Tensor, nbases: int) -> np.ndarray:
     w = sign.cpu().numpy().view(np.uint32)
     bits = ((w[:, None] >> np.arange(32, dtype=np.uint32)[None, :]) & 1).astype(np.uint8)
     return bits.ravel()[:nbases]
+
+
+INGEST_RESULT_N = 8   # int64 fields of cpg_ingest_result
+
+
+def text_to_device(txt: bytes, device) -> torch.Tensor:
+    """Raw text bytes as a uint8 device tensor (16-byte aligned by the allocator)."""
+    return torch.frombuffer(bytearray(txt) or bytearray(1), dtype=torch.uint8).to(device)
+
+
+def ingest(ctx: Context, d_txt: torch.Tensor, n: int, mode: int, compat_quirks: bool = True,
+           cap_bases: int | None = None, out: torch.Tensor | None = None,
+           result: torch.Tensor | None = None):
+    """Device-side reader (cpg_ingest_d): raw text in HBM -> packed committed chunks.
+
+    Returns (packed int32 tensor, result int64[8] tensor = cpg_ingest_result), asynchronous
+    on the current stream.  cap_bases defaults to n plus 1/8 slack for the training
+    reader's extra all-A chunks (a FASTA file whose line cadence meets the chunk cadence gets
+    one every few chunks), rounded to whole chunks; result[1] reports CPG_E_CAPACITY."""
+    chunk = _lib.TRAIN_CHUNK if mode == 0 else _lib.DECODE_CHUNK
+    if cap_bases is None:
+        cap_bases = ((n + n // 8) // chunk + 8) * chunk
+    if out is None:
+        out = torch.empty(words16(cap_bases) + 4, dtype=torch.int32, device=d_txt.device)
+    if result is None:
+        result = torch.empty(INGEST_RESULT_N, dtype=torch.int64, device=d_txt.device)
+    check(lib.cpg_ingest_d(ctx.handle, _dp(d_txt), n, mode, int(bool(compat_quirks)), _dp(out),
+                           cap_bases, _dp(result), _stream()))
+    return out, result

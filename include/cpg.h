@@ -180,6 +180,24 @@ int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_s
                      int64_t nbases, int64_t chunk_len, int64_t first_chunk,
                      cpg_island* d_out, int64_t cap, int64_t* d_count, void* stream);
 
+/* Device-side ASCII ingest: the reference's readers (CpGIslandFinder.java:112-145, mode 0 =
+ * training; :238-259, mode 1 = decode) over raw text already in HBM, with exactly the
+ * semantics of cpg_ingest (same quirks, same committed prefix, same error rules).  d_txt:
+ * 16-byte aligned.  d_packed: capacity cap_bases bases (zeroed, then written; bases past the
+ * last committed chunk may be written too, as by cpg_ingest).  *d_result (device memory)
+ * receives the outcome: asynchronous on `stream`, like every "_d" entry point. */
+typedef struct cpg_ingest_result {
+    int64_t nbases;        /* committed bases (whole chunks), cpg_ingest's *nbases */
+    int64_t status;        /* CPG_OK, CPG_E_REF_CRASH, CPG_E_CAPACITY or CPG_E_DEVICE */
+    int64_t crash_byte;    /* input byte at which the reference throws, else -1 */
+    int64_t valid_bases;   /* ACGT bytes in the text */
+    int64_t extra_chunks;  /* all-A chunks the training reader inserts (:130-141 quirk) */
+    int64_t reserved[3];
+} cpg_ingest_result;
+int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compat_quirks,
+                 uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result,
+                 void* stream);
+
 /* ---- host-buffer entry points (stage through pinned memory, synchronous) ------- */
 int cpg_count_labelled(cpg_ctx* ctx, const uint32_t* packed, const uint32_t* sign,
                        int64_t nbases, int64_t chunk_len, cpg_counts_i64* out);
@@ -192,6 +210,10 @@ int cpg_viterbi(cpg_ctx* ctx, const cpg_model* model, const uint32_t* packed,
  * states_out[i] in 0..7. */
 int cpg_decode_states(cpg_ctx* ctx, const cpg_model* model, const int32_t* obs,
                       int64_t n, int32_t* states_out);
+/* cpg_ingest computed on the GPU: host text staged through pinned memory, the packed
+ * chunks copied back.  Same arguments, results and return codes as cpg_ingest. */
+int cpg_ingest_gpu(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat_quirks,
+                   uint32_t* packed, int64_t cap_bases, int64_t* nbases);
 int cpg_islands(cpg_ctx* ctx, const uint32_t* packed, const uint32_t* sign,
                 int64_t nbases, int64_t chunk_len, cpg_island* out, int64_t cap,
                 int64_t* count);
