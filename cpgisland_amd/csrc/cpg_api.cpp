@@ -49,12 +49,12 @@ int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
 
 namespace {
 
-enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
-       WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9 };
 
 // NULL is the HIP null stream (torch's default stream handle is 0 too); the host-buffer
 // wrappers pass the context's own stream explicitly
 hipStream_t pick(cpg_ctx*, void* stream) { return static_cast<hipStream_t>(stream); }
+
+}  // namespace
 
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
@@ -79,6 +79,8 @@ int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitT
     *out = sl->d;
     return CPG_OK;
 }
+
+namespace {
 
 int check_layout(const void* packed, int64_t nbases, int64_t chunk_len) {
     if (!packed && nbases > 0) return set_error(CPG_E_INVALID, "null packed buffer");
@@ -129,6 +131,10 @@ void cpg_close(cpg_ctx* ctx) {
         if (b.p) (void)hipHostFree(b.p);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     for (int i = 0; i < ctx->vtn; ++i) (void)hipFree(ctx->vtc[i].d);
+    for (auto& ps : ctx->ps)
+        if (ps) (void)hipStreamDestroy(ps);
+    for (auto& ev : ctx->pev)
+        if (ev) (void)hipEventDestroy(ev);
     (void)hipStreamDestroy(ctx->stream);
     delete ctx;
 }

@@ -84,17 +84,31 @@ struct cpg_ctx {
         cpg::VitTables* d;
     } vtc[kVtSlots];
     int vtn = 0, vtnext = 0;
+    // streamed-genome pipeline (cpg_genome_run): copy-in, train, decode, copy-out streams
+    // and per-buffer events, created on first use
+    hipStream_t ps[4] = {};
+    static constexpr int kMaxBuf = 8;
+    hipEvent_t pev[4 * kMaxBuf] = {};
 };
 
 namespace cpg {
 int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out);
 int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out);
 int model_check_deterministic(const cpg_model* m);
+bool aligned16(const void* p);
+int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitTables** out);
+enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
+       WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9, WS_GEN = 10, WS_GISL = 11 };
 int vit_prepare(const cpg_model* m, int64_t chunk_len, VitConsts* vc, VitTables* vt);
 
 // kernel launchers (defined in the .hip files); all asynchronous on `s`
+// parts: bit 0 = accumulate the chunks into the context's fixed-point accumulators, bit 1 =
+// finalize (convert to the output struct and re-zero).  A streamed genome accumulates every
+// window and finalizes once: bit-identical to one call over the whole genome.
+enum { PART_ACC = 1, PART_FINAL = 2, PART_ALL = 3 };
 hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
-                        int64_t chunk_len, uint64_t* ws, int64_t* out /*124*/, hipStream_t s);
+                        int64_t chunk_len, uint64_t* ws, int64_t* out /*124*/, hipStream_t s,
+                        int parts = PART_ALL);
 size_t count_ws_bytes(int64_t nchunks);
 hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint32_t* packed,
                           int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
@@ -104,11 +118,12 @@ size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len);
 int64_t vit_nsb(int64_t chunk_len);
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* ws, size_t ws_bytes,
-                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s);
+                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s,
+                          const int64_t* base_in = nullptr);
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t chunk_len, unsigned long long* acc, double* out,
-                        hipStream_t s);
+                        hipStream_t s, int parts = PART_ALL);
 size_t estep_ws_bytes(int64_t nchunks, int64_t chunk_len);
 
 hipError_t launch_ingest(const uint8_t* txt, int64_t n, int mode, int quirks, int64_t chunk,

@@ -218,15 +218,19 @@ __device__ void final_counts(const uint64_t* raw, int t, int64_t* __restrict__ o
 }  // namespace
 
 hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
-                        int64_t chunk_len, uint64_t* ws, int64_t* out, hipStream_t s) {
+                        int64_t chunk_len, uint64_t* ws, int64_t* out, hipStream_t s, int parts) {
     const int64_t nblk = nchunks * chunk_len / 64;
-    if (nblk <= 0) return hipMemsetAsync(out, 0, 124 * sizeof(int64_t), s);
-    int grid = 1024;
-    if ((int64_t)grid * kCountThreads > nblk) grid = (int)((nblk + kCountThreads - 1) / kCountThreads);
-    hipLaunchKernelGGL(k_count_main, dim3(grid), dim3(kCountThreads), 0, s,
-                       (const uint4*)packed, (const uint2*)sign, packed, sign, nblk,
-                       chunk_len / 64, (unsigned long long*)ws);
-    hipLaunchKernelGGL(k_count_final, dim3(1), dim3(128), 0, s, (unsigned long long*)ws, out);
+    if (nblk <= 0 && parts == PART_ALL) return hipMemsetAsync(out, 0, 124 * sizeof(int64_t), s);
+    if ((parts & PART_ACC) && nblk > 0) {
+        int grid = 1024;
+        if ((int64_t)grid * kCountThreads > nblk)
+            grid = (int)((nblk + kCountThreads - 1) / kCountThreads);
+        hipLaunchKernelGGL(k_count_main, dim3(grid), dim3(kCountThreads), 0, s,
+                           (const uint4*)packed, (const uint2*)sign, packed, sign, nblk,
+                           chunk_len / 64, (unsigned long long*)ws);
+    }
+    if (parts & PART_FINAL)
+        hipLaunchKernelGGL(k_count_final, dim3(1), dim3(128), 0, s, (unsigned long long*)ws, out);
     return hipGetLastError();
 }
 

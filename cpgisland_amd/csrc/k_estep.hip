@@ -528,16 +528,21 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
 size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8; }
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
-                        int64_t C, unsigned long long* acc, double* out, hipStream_t s) {
+                        int64_t C, unsigned long long* acc, double* out, hipStream_t s,
+                        int parts) {
     if (C % 4096 || C > (int64_t)kET * kLanePos) return hipErrorInvalidValue;
-    if (nchunks == 0) return hipMemsetAsync(out, 0, 105 * sizeof(double), s);
-    const int lanes = (int)(C / kLanePos);
-    const size_t uni = kUnionBytes;   // sized for 16 waves; fewer lanes use a prefix
-    const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long) +
-                       (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
-    hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
-                       packed, C, acc);
-    hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);
+    if (nchunks == 0 && parts == PART_ALL)
+        return hipMemsetAsync(out, 0, 105 * sizeof(double), s);
+    if ((parts & PART_ACC) && nchunks > 0) {
+        const int lanes = (int)(C / kLanePos);
+        const size_t uni = kUnionBytes;   // sized for 16 waves; fewer lanes use a prefix
+        const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long) +
+                           (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
+        hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
+                           packed, C, acc);
+    }
+    if (parts & PART_FINAL)
+        hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);
     return hipGetLastError();
 }
 

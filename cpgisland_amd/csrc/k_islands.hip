@@ -369,7 +369,8 @@ __global__ __launch_bounds__(kIT) void k_isl_b(const uint32_t* packed, const uin
 
 __global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, const uint32_t* sign,
                                                int64_t C, int64_t first_chunk, IslWs ws,
-                                               cpg_island* out, int64_t cap, int64_t* count) {
+                                               cpg_island* out, int64_t cap, int64_t* count,
+                                               const int64_t* base_in) {
     const int64_t c = blockIdx.x;
     // the chunk's first record: kept islands of all earlier chunks (fixed-order sum)
     __shared__ int64_t sb[kIT];
@@ -383,7 +384,9 @@ __global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, const uin
             __syncthreads();
         }
     }
-    const int64_t base = sb[0];
+    // append mode (streamed windows): records continue after *base_in earlier ones and
+    // *count receives the running total
+    const int64_t base = sb[0] + (base_in ? *base_in : 0);
     if (c == (int64_t)gridDim.x - 1 && threadIdx.x == 0) *count = base + ws.nkept[c];
     const int64_t nw = C / 32, maxr = C / 2 + 1;
     const uint32_t* pk = packed + c * (C / 16);
@@ -420,10 +423,13 @@ size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len) {
 
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* wsp, size_t ws_bytes,
-                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s) {
+                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s,
+                          const int64_t* base_in) {
     IslWs ws = carve_isl(wsp, nchunks, chunk_len);
     if (ws.bytes > ws_bytes) return hipErrorInvalidValue;
-    if (nchunks == 0) return hipMemsetAsync(count, 0, sizeof(int64_t), s);
+    if (nchunks == 0)
+        return base_in ? hipMemcpyAsync(count, base_in, sizeof(int64_t), hipMemcpyDeviceToDevice, s)
+                       : hipMemsetAsync(count, 0, sizeof(int64_t), s);
     const int ntiles = (int)((chunk_len / 32 + kTileW - 1) / kTileW);
     Cnt5* tiles = static_cast<Cnt5*>(ws.tiles);
     hipLaunchKernelGGL(k_isl_a1, dim3((unsigned)(nchunks * ntiles)), dim3(kAT), 0, s, packed,
@@ -433,7 +439,7 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
     hipLaunchKernelGGL(k_isl_b, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
                        chunk_len, ws);
     hipLaunchKernelGGL(k_isl_d, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
-                       chunk_len, first_chunk, ws, out, cap, count);
+                       chunk_len, first_chunk, ws, out, cap, count, base_in);
     return hipGetLastError();
 }
 

@@ -131,3 +131,38 @@ def ingest(ctx: Context, d_txt: torch.Tensor, n: int, mode: int, compat_quirks: 
     check(lib.cpg_ingest_d(ctx.handle, _dp(d_txt), n, mode, int(bool(compat_quirks)), _dp(out),
                            cap_bases, _dp(result), _stream()))
     return out, result
+
+
+def genome_run(ctx: Context, train_model: HmmModel | None, decode_model: HmmModel | None,
+               packed: np.ndarray, sign: np.ndarray | None, nbases: int,
+               window_bases: int = 0, nbuf: int = 0, want_sign_out: bool = True,
+               island_cap: int = 1 << 20):
+    """Streamed whole-genome pass from HOST memory (cpg_genome_run, BASELINE config C5).
+
+    Returns a dict: estep (105 doubles) | counts (124 int64) | sign_out (uint32 words) |
+    scores (per decode chunk) | islands (records)."""
+    assert packed.dtype == np.uint32 and packed.flags["C_CONTIGUOUS"]
+    opts = np.zeros(2, np.int64)
+    opts[0] = window_bases
+    opts[1] = nbuf            # nbuf (int32) + reserved (int32), little endian
+    est = np.zeros(_lib.COUNTS_F64_N, np.float64) if train_model is not None else None
+    cnt = np.zeros(_lib.COUNTS_I64_N, np.int64) if sign is not None else None
+    ndec = nbases // _lib.DECODE_CHUNK
+    sg = np.zeros(words32(nbases) + 1, np.uint32) if (decode_model is not None and
+                                                       want_sign_out) else None
+    sc = np.zeros(max(ndec, 1), np.float64) if decode_model is not None else None
+    isl = np.zeros(max(island_cap, 1), _lib.ISLAND_DTYPE) if decode_model is not None else None
+    icount = C.c_int64(0)
+    tm = train_model.to_struct() if train_model is not None else None
+    dm = decode_model.to_struct() if decode_model is not None else None
+
+    def p(a):
+        return ptr(a) if a is not None else None
+
+    check(lib.cpg_genome_run(ctx.handle, p(tm), p(dm), ptr(packed),
+                             p(sign) if sign is not None else None, nbases, ptr(opts),
+                             p(est), p(cnt), p(sg), p(sc), p(isl), island_cap if isl is not None
+                             else 0, C.byref(icount) if dm is not None else None))
+    return {"estep": est, "counts": cnt, "sign_out": sg, "scores": sc[:ndec] if sc is not None
+            else None, "islands": isl[:icount.value] if isl is not None else None,
+            "island_count": icount.value}

@@ -198,6 +198,32 @@ int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compa
                  uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result,
                  void* stream);
 
+/* ---- streamed whole-genome pass (host memory -> HBM, overlapped) ---------------- */
+/* One training + decode pass over a genome in HOST memory, streamed to the device in windows
+ * of whole 1 Mi chunks (BASELINE config C5): H2D copies of window k+1 overlap the E-step /
+ * labelled counts (train stream) and the Viterbi / island scan (decode stream) of window k,
+ * and the D2H of the decoded path.  It is the reference's trainModel mapper pass (:130-141,
+ * :200) and testModel (:256-339) for one genome in one call, with results identical to the
+ * "_d" entry points over the whole genome at once (the E-step and count accumulators are
+ * fixed point and finalized once; island records are appended in chunk order).
+ *   train_model  : E-step model (NULL: no E-step; estep_out must then be NULL)
+ *   decode_model : Viterbi model (NULL: no decode)
+ *   sign         : truth labels for the labelled counts (NULL: none; counts_out NULL)
+ *   sign_out     : decoded path as sign bits (NULL: not returned); the tail reads '-'
+ *   score_out    : best log-probability per decode chunk (NULL: not returned)
+ *   islands_out / island_cap / island_count : as cpg_islands (CPG_E_CAPACITY if exceeded)
+ * Host buffers that are not pinned are page-locked for the duration of the call. */
+typedef struct cpg_genome_opts {
+    int64_t window_bases;   /* multiple of CPG_DECODE_CHUNK; 0: 64 Mi */
+    int     nbuf;           /* device window buffers, 2..8; 0: 3 */
+    int     reserved;
+} cpg_genome_opts;
+int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model, const cpg_model* decode_model,
+                   const uint32_t* packed, const uint32_t* sign, int64_t nbases,
+                   const cpg_genome_opts* opts, cpg_counts_f64* estep_out,
+                   cpg_counts_i64* counts_out, uint32_t* sign_out, double* score_out,
+                   cpg_island* islands_out, int64_t island_cap, int64_t* island_count);
+
 /* ---- host-buffer entry points (stage through pinned memory, synchronous) ------- */
 int cpg_count_labelled(cpg_ctx* ctx, const uint32_t* packed, const uint32_t* sign,
                        int64_t nbases, int64_t chunk_len, cpg_counts_i64* out);
