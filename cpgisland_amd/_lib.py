@@ -77,6 +77,11 @@ SIGNATURES = {
     "cpg_ingest_d": [_P, _P, _I64, _INT, _INT, _P, _I64, _P, _P],
     "cpg_ingest_gpu": [_P, C.c_char_p, C.c_size_t, _INT, _INT, _P, _I64, _P],
     "cpg_genome_run": [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _I64, _P],
+    "cpg_contigs_order_d": [_P, _P, _I64, _P, _P],
+    "cpg_contigs_count_labelled_d": [_P, _P, _P, _I64, _P, _P, _P, _I64, _P, _P],
+    "cpg_contigs_estep_d": [_P, _P, _P, _I64, _P, _P, _P, _I64, _P, _P],
+    "cpg_contigs_viterbi_d": [_P, _P, _P, _I64, _P, _P, _P, _I64, _P, _P, _P],
+    "cpg_contigs_islands_d": [_P, _P, _P, _I64, _P, _P, _P, _I64, _P, _I64, _P, _P],
 }
 
 

@@ -163,11 +163,16 @@ int cpg_sync(cpg_ctx* ctx, void* stream) {
     if (st) {
         CPG_HIP(hipMemsetAsync(ctx->d_status, 0, 4, s));
         CPG_HIP(hipStreamSynchronize(s));
+        if (st == ST_CONTIG_LAYOUT)
+            return set_error(CPG_E_INVALID,
+                             "contig batch: a contig breaks the layout contract (offset %% 64, "
+                             "length >= 1 (<= 2^20 for the E-step), inside nbases); skipped");
         return set_error(CPG_E_VERIFY,
-                         "kernel self-check failed (status 0x%x: %s%s%s)", st,
+                         "kernel self-check failed (status 0x%x: %s%s%s%s)", st,
                          (st & ST_VERIFY_ENTRY) ? "viterbi block exit != next entry; " : "",
                          (st & ST_VERIFY_MAG) ? "composite out of exact range; " : "",
-                         (st & ST_VERIFY_CHAIN) ? "traceback chain mismatch" : "");
+                         (st & ST_VERIFY_CHAIN) ? "traceback chain mismatch; " : "",
+                         (st & ST_CONTIG_LAYOUT) ? "contig layout contract broken" : "");
     }
     return CPG_OK;
 }

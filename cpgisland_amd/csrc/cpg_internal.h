@@ -30,6 +30,7 @@ enum : uint32_t {
     ST_VERIFY_ENTRY = 1u << 0,   // K5 exit value != K4 entry of the next block
     ST_VERIFY_MAG = 1u << 1,     // K3 composite outside the exact range
     ST_VERIFY_CHAIN = 1u << 2,   // K7 traceback start state mismatch
+    ST_CONTIG_LAYOUT = 1u << 3,  // a contig breaks the batch layout contract (skipped)
 };
 
 // ---- Viterbi constants (host-computed, shared by every kernel) ---------------------
@@ -98,7 +99,8 @@ int model_check_deterministic(const cpg_model* m);
 bool aligned16(const void* p);
 int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitTables** out);
 enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
-       WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9, WS_GEN = 10, WS_GISL = 11 };
+       WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9, WS_GEN = 10, WS_GISL = 11, WS_CSORT = 12,
+       WS_CBP = 13, WS_CISL = 14, WS_CCK = 15 };
 int vit_prepare(const cpg_model* m, int64_t chunk_len, VitConsts* vc, VitTables* vt);
 
 // kernel launchers (defined in the .hip files); all asynchronous on `s`
@@ -125,6 +127,27 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
                         int64_t chunk_len, unsigned long long* acc, double* out,
                         hipStream_t s, int parts = PART_ALL);
 size_t estep_ws_bytes(int64_t nchunks, int64_t chunk_len);
+
+// ragged contig batches (k_contigs.hip)
+size_t contigs_sort_ws_bytes(int64_t n);
+hipError_t launch_contigs_order(const int32_t* lens, int64_t n, int32_t* order, void* ws,
+                                size_t ws_bytes, hipStream_t s);
+hipError_t launch_contigs_count(const uint32_t* packed, const uint32_t* sign, int64_t nbases,
+                                const int64_t* offs, const int32_t* lens, const int32_t* order,
+                                int64_t n, uint64_t* ws, int64_t* out, uint32_t* status,
+                                hipStream_t s);
+hipError_t launch_contigs_viterbi(const VitConsts& vc, const uint32_t* packed, int64_t nbases,
+                                  const int64_t* offs, const int32_t* lens, const int32_t* order,
+                                  int64_t n, uint32_t* bp, uint32_t* sign_out, double* score,
+                                  uint32_t* status, hipStream_t s);
+hipError_t launch_contigs_estep(const cpg_model& model, const uint32_t* packed, int64_t nbases,
+                                const int64_t* offs, const int32_t* lens, const int32_t* order,
+                                int64_t n, void* ck, unsigned long long* acc, double* out,
+                                uint32_t* status, hipStream_t s);
+hipError_t launch_contigs_islands(const uint32_t* packed, const uint32_t* sign, int64_t nbases,
+                                  const int64_t* offs, const int32_t* lens, const int32_t* order,
+                                  int64_t n, void* ws, size_t ws_bytes, cpg_island* out,
+                                  int64_t cap, int64_t* count, uint32_t* status, hipStream_t s);
 
 hipError_t launch_ingest(const uint8_t* txt, int64_t n, int mode, int quirks, int64_t chunk,
                          uint32_t* out, int64_t cap, void* ws, size_t ws_bytes,

@@ -166,3 +166,69 @@ def genome_run(ctx: Context, train_model: HmmModel | None, decode_model: HmmMode
     return {"estep": est, "counts": cnt, "sign_out": sg, "scores": sc[:ndec] if sc is not None
             else None, "islands": isl[:icount.value] if isl is not None else None,
             "island_count": icount.value}
+
+
+# ---- ragged contig batches (BASELINE config C4) ------------------------------------------
+def contig_layout(lens: np.ndarray, gap: int = 0):
+    """64-aligned offsets for contigs of the given lengths packed back to back (plus `gap`
+    bases between them): (offs int64[n], nbases span)."""
+    lens = np.asarray(lens, np.int64)
+    step = (lens + gap + 63) // 64 * 64
+    offs = np.zeros(len(lens), np.int64)
+    if len(lens) > 1:
+        offs[1:] = np.cumsum(step)[:-1]
+    span = int(offs[-1] + lens[-1]) if len(lens) else 0
+    return offs, span
+
+
+def contigs_order(ctx: Context, lens: torch.Tensor, n: int, out: torch.Tensor | None = None):
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.int32, device=lens.device)
+    check(lib.cpg_contigs_order_d(ctx.handle, _dp(lens), n, _dp(out), _stream()))
+    return out
+
+
+def _opt(t):
+    return _dp(t) if t is not None else None
+
+
+def contigs_count_labelled(ctx, packed, sign, nbases, offs, lens, order, n, out=None):
+    if out is None:
+        out = torch.empty(_lib.COUNTS_I64_N, dtype=torch.int64, device=packed.device)
+    check(lib.cpg_contigs_count_labelled_d(ctx.handle, _dp(packed), _dp(sign), nbases, _dp(offs),
+                                           _dp(lens), _opt(order), n, _dp(out), _stream()))
+    return out
+
+
+def contigs_estep(ctx, model: HmmModel, packed, nbases, offs, lens, order, n, out=None):
+    if out is None:
+        out = torch.empty(_lib.COUNTS_F64_N, dtype=torch.float64, device=packed.device)
+    m = model.to_struct()
+    check(lib.cpg_contigs_estep_d(ctx.handle, ptr(m), _dp(packed), nbases, _dp(offs), _dp(lens),
+                                  _opt(order), n, _dp(out), _stream()))
+    return out
+
+
+def contigs_viterbi(ctx, model: HmmModel, packed, nbases, offs, lens, order, n,
+                    sign_out=None, score=None):
+    if sign_out is None:
+        sign_out = torch.zeros(words32(nbases) + 4, dtype=torch.int32, device=packed.device)
+    if score is None:
+        score = torch.empty(max(n, 1), dtype=torch.float64, device=packed.device)
+    m = model.to_struct()
+    check(lib.cpg_contigs_viterbi_d(ctx.handle, ptr(m), _dp(packed), nbases, _dp(offs), _dp(lens),
+                                    _opt(order), n, _dp(sign_out), _dp(score), _stream()))
+    return sign_out, score
+
+
+def contigs_islands(ctx, packed, sign, nbases, offs, lens, order, n, cap=1 << 20, out=None,
+                    count=None):
+    if out is None:
+        out = torch.empty((max(cap, 1), _lib.ISLAND_DTYPE.itemsize), dtype=torch.uint8,
+                          device=packed.device)
+    if count is None:
+        count = torch.zeros(1, dtype=torch.int64, device=packed.device)
+    check(lib.cpg_contigs_islands_d(ctx.handle, _dp(packed), _dp(sign), nbases, _dp(offs),
+                                    _dp(lens), _opt(order), n, _dp(out), cap, _dp(count),
+                                    _stream()))
+    return out, count

@@ -198,6 +198,44 @@ int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compa
                  uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result,
                  void* stream);
 
+/* ---- ragged contig batches (BASELINE config C4) ------------------------------------ */
+/* A batch of independent sequences in ONE packed buffer of nbases bases: contig c occupies
+ * bases [offs[c], offs[c] + lens[c]), offs[c] % 64 == 0 (each contig starts a 64-base block:
+ * aligned 16-B loads, whole sign words of its own), lens[c] >= 1, contigs not overlapping.
+ * Build-defined batch semantics: every contig is one observation sequence exactly as one
+ * whole chunk is in the reference (training :130-141 -> BW mapper :200; decode :256-260 ->
+ * HmmEvaluator.decode; islands :262-339 with the contig as the chunk).  d_offs int64[n],
+ * d_lens int32[n], device.  A contig breaking the contract is skipped and cpg_sync reports
+ * CPG_E_INVALID.
+ * d_order (may be NULL = batch order): the wavefront schedule from cpg_contigs_order_d —
+ * contig indices by decreasing length, so the 64 lanes of a wave (one contig each) have
+ * nearly equal work.  Results never depend on the order. */
+int cpg_contigs_order_d(cpg_ctx* ctx, const int32_t* d_lens, int64_t n, int32_t* d_order,
+                        void* stream);
+/* labelled counts over all contigs (init = each contig's first base); as cpg_count_labelled_d */
+int cpg_contigs_count_labelled_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
+                                 int64_t nbases, const int64_t* d_offs, const int32_t* d_lens,
+                                 const int32_t* d_order, int64_t n, int64_t* d_counts,
+                                 void* stream);
+/* Baum-Welch E-step summed over contigs (each contig <= 1,048,576 bases); as cpg_bw_estep_d */
+int cpg_contigs_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                        int64_t nbases, const int64_t* d_offs, const int32_t* d_lens,
+                        const int32_t* d_order, int64_t n, double* d_counts, void* stream);
+/* exact Viterbi per contig: sign bits at the contig's own bit positions of d_sign_out (a
+ * buffer shaped like the packed span, 32 bases per word; bits past a contig's end are '-'),
+ * best log-probability per contig in d_score[c] (may be NULL).  Model contract as
+ * cpg_viterbi_d. */
+int cpg_contigs_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                          int64_t nbases, const int64_t* d_offs, const int32_t* d_lens,
+                          const int32_t* d_order, int64_t n, uint32_t* d_sign_out,
+                          double* d_score, void* stream);
+/* island scan per contig: records in contig order, beg1/end1 1-based within the contig,
+ * `chunk` = contig index; an island open at a contig's end is dropped (as at a chunk end). */
+int cpg_contigs_islands_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
+                          int64_t nbases, const int64_t* d_offs, const int32_t* d_lens,
+                          const int32_t* d_order, int64_t n, cpg_island* d_out, int64_t cap,
+                          int64_t* d_count, void* stream);
+
 /* ---- streamed whole-genome pass (host memory -> HBM, overlapped) ---------------- */
 /* One training + decode pass over a genome in HOST memory, streamed to the device in windows
  * of whole 1 Mi chunks (BASELINE config C5): H2D copies of window k+1 overlap the E-step /
