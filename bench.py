@@ -129,6 +129,10 @@ def main():
                     help="1: decode stream at high priority (two-stream mode)")
     ap.add_argument("--serial", action="store_true",
                     help="train and decode phases on one stream (isolated phase timing)")
+    ap.add_argument("--no-overlap", action="store_true",
+                    help="join both streams after every step (by default step k+1's training "
+                         "pass may start while step k's decode still runs: the steps are "
+                         "independent batches, pipelined for throughput)")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="write this many MiB of scratch between steps (cold Infinity Cache)")
     args = ap.parse_args()
@@ -186,7 +190,9 @@ def main():
 
     # The training pass and the decode are independent within a step: by default they run
     # concurrently on two streams (the decode kernels are latency-bound and leave SIMDs idle
-    # that the E-step fills).  --serial runs everything on one stream (isolated phase times).
+    # that the E-step fills), and consecutive steps (independent batches) are pipelined: no
+    # join between steps (--no-overlap adds one).  --serial runs everything on one stream
+    # (isolated phase times).
     main_s = torch.cuda.current_stream()
     s_tr = main_s if args.serial else torch.cuda.Stream()
     # the decode stream at high priority: its latency-bound kernels get CUs first as the
@@ -197,8 +203,9 @@ def main():
         def mark(k, i):
             if it is not None:
                 evs[it][k][i].record()
-        s_tr.wait_stream(main_s)
-        s_dec.wait_stream(main_s)
+        if args.no_overlap or args.serial:
+            s_tr.wait_stream(main_s)
+            s_dec.wait_stream(main_s)
         with torch.cuda.stream(s_dec):
             mark("viterbi", 0)
             D.viterbi(ctx, model1, dp, N, DECODE, sign_out=so, score=score)
@@ -219,8 +226,9 @@ def main():
                 cdist.merge_counts_i64(lcnt)
                 cdist.merge_counts_f64(ecnt)
             mark("reduce", 1)
-        main_s.wait_stream(s_tr)
-        main_s.wait_stream(s_dec)
+        if args.no_overlap or args.serial:
+            main_s.wait_stream(s_tr)
+            main_s.wait_stream(s_dec)
 
     for _ in range(args.warmup):
         step(None)
@@ -236,6 +244,8 @@ def main():
         if flush is not None:
             flush.fill_(1.0)
         step(it)
+    main_s.wait_stream(s_tr)
+    main_s.wait_stream(s_dec)
     torch.cuda.synchronize()
     for ev in evs:
         for k, (a, b) in ev.items():
@@ -289,6 +299,7 @@ def main():
                                       "counts + RCCL reduce + exact Viterbi + islands",
                           "streams": 1 if args.serial else 2,
                           "decode_priority": "high" if (args.prio and not args.serial) else "normal",
+                          "step_overlap": not (args.no_overlap or args.serial),
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
                           "islands_found": int(icnt.item())},
