@@ -78,6 +78,8 @@ SIGNATURES = {
     "cpg_ingest_gpu": [_P, C.c_char_p, C.c_size_t, _INT, _INT, _P, _I64, _P],
     "cpg_genome_run": [_P, _P, _P, _P, _P, _I64, _P, _P, _P, _P, _P, _P, _I64, _P],
     "cpg_contigs_order_d": [_P, _P, _I64, _P, _P],
+    "cpg_format_islands": [_P, _I64, _P, _I64, _P],
+    "cpg_format_model": [_P, _P, _I64, _P],
     "cpg_contigs_count_labelled_d": [_P, _P, _P, _I64, _P, _P, _P, _I64, _P, _P],
     "cpg_contigs_estep_d": [_P, _P, _P, _I64, _P, _P, _P, _I64, _P, _P],
     "cpg_contigs_viterbi_d": [_P, _P, _P, _I64, _P, _P, _P, _I64, _P, _P, _P],

@@ -130,3 +130,28 @@ class HmmEvaluator:
         check(lib.cpg_decode_states(ctx.handle, ptr(m), ptr(obs) if len(obs) else None,
                                     len(obs), ptr(out)))
         return out[: len(obs)]
+
+
+def format_islands(records) -> bytes:
+    """The island file lines of CpGIslandFinder.java:287-288, byte-exact (cpg_format_islands)."""
+    import ctypes as C
+
+    from ._lib import ISLAND_DTYPE, check, lib, ptr
+    recs = np.ascontiguousarray(records, dtype=ISLAND_DTYPE)
+    need = C.c_int64(0)
+    cap = max(64, len(recs) * 64)
+    buf = C.create_string_buffer(cap)
+    check(lib.cpg_format_islands(ptr(recs) if len(recs) else None, len(recs), buf, cap,
+                                 C.byref(need)))
+    return buf.raw[:need.value]
+
+
+def format_model(model: "HmmModel") -> bytes:
+    """The trained-model file of CpGIslandFinder.java:207-224, byte-exact (cpg_format_model)."""
+    import ctypes as C
+
+    from ._lib import check, lib, ptr
+    need = C.c_int64(0)
+    buf = C.create_string_buffer(8192)
+    check(lib.cpg_format_model(ptr(model.to_struct()), buf, 8192, C.byref(need)))
+    return buf.raw[:need.value]

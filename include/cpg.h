@@ -142,6 +142,19 @@ int cpg_bw_normalize(const cpg_counts_f64* counts, cpg_model* out);
 /* Labelled-count M-step (same normalisation over the integer counts). */
 int cpg_counts_normalize(const cpg_counts_i64* counts, cpg_model* out);
 
+/* The reference's text outputs, byte-exact (Java rendering of doubles: shortest
+ * round-trip digits; root locale).  Both return CPG_E_CAPACITY with *nbytes = the size
+ * needed when cap is too small.  No terminating NUL is written.
+ *   cpg_format_islands: one line per record, String.format("%d %d %d %f %f\n", beg1, end1,
+ *                       len, cg, oe) as at CpGIslandFinder.java:287-288 (%f: HALF_UP on
+ *                       the shortest digits);
+ *   cpg_format_model  : the trained-model file of :207-224: per state i, Double.toString
+ *                       of pi[i], newline, a[i][0..7] each followed by " ", newline,
+ *                       b[i][0..3] each followed by " ", newline. */
+int cpg_format_islands(const cpg_island* recs, int64_t n, char* buf, int64_t cap,
+                       int64_t* nbytes);
+int cpg_format_model(const cpg_model* model, char* buf, int64_t cap, int64_t* nbytes);
+
 /* ---- device path: HBM-resident inputs (device pointers), async on `stream` ----- */
 
 /* Labelled counts over whole chunk_len chunks (tail dropped).  d_counts: device

@@ -219,7 +219,48 @@ def islands(states, chunk: int):
 def java_f6(x: float) -> str:
     """java.util.Formatter '%f': shortest round-trip digits (repr), HALF_UP to 6."""
     from decimal import ROUND_HALF_UP, Decimal
+    x = float(x)
     return str(Decimal(repr(x)).quantize(Decimal("0.000001"), rounding=ROUND_HALF_UP))
+
+
+def java_dtoa(x: float) -> str:
+    """java.lang.Double.toString (JDK 19+ spec: shortest round-trip digits, `repr`'s):
+    plain decimal for 1e-3 <= |x| < 1e7 with at least one fraction digit, else
+    d.ddd...E[-]n.  Used for the trained-model file of CpGIslandFinder.java:207-224."""
+    import math
+    from decimal import Decimal
+    x = float(x)
+    if math.isnan(x):
+        return "NaN"
+    if math.isinf(x):
+        return "Infinity" if x > 0 else "-Infinity"
+    sign = "-" if math.copysign(1.0, x) < 0 else ""
+    if x == 0.0:
+        return sign + "0.0"
+    t = Decimal(repr(abs(x))).as_tuple()
+    digits = "".join(map(str, t.digits)).rstrip("0") or "0"
+    e = t.exponent + len(t.digits)            # value = 0.digits x 10^e
+    if 1e-3 <= abs(x) < 1e7:
+        if e > 0:
+            ip = (digits + "0" * e)[:e]
+            fp = digits[e:]
+        else:
+            ip, fp = "0", "0" * (-e) + digits
+        return sign + ip + "." + (fp or "0")
+    return sign + digits[0] + "." + (digits[1:] or "0") + "E" + str(e - 1)
+
+
+def format_model(m) -> str:
+    """The trained-model file (:207-224) for a 104-double model pi|a|b."""
+    import numpy as np
+    m = np.asarray(m, np.float64)
+    pi, a, b = m[:8], m[8:72].reshape(8, 8), m[72:104].reshape(8, 4)
+    out = []
+    for i in range(8):
+        out.append(java_dtoa(pi[i]) + "\n")
+        out.append("".join(java_dtoa(v) + " " for v in a[i]) + "\n")
+        out.append("".join(java_dtoa(v) + " " for v in b[i]) + "\n")
+    return "".join(out)
 
 
 def format_island(rec) -> str:
