@@ -84,6 +84,8 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
     const int64_t D = CPG_DECODE_CHUNK, T = CPG_TRAIN_CHUNK;
     int64_t W = opts && opts->window_bases > 0 ? opts->window_bases : 64 * D;
     int nbuf = opts && opts->nbuf > 0 ? opts->nbuf : 3;
+    const int64_t chunk0 = opts ? opts->first_chunk : 0;
+    if (chunk0 < 0) return set_error(CPG_E_INVALID, "first_chunk < 0");
     if (W % D) return set_error(CPG_E_INVALID, "window_bases must be a multiple of 1,048,576");
     if (nbuf < 2 || nbuf > cpg_ctx::kMaxBuf)
         return set_error(CPG_E_INVALID, "nbuf must be in 2..%d", cpg_ctx::kMaxBuf);
@@ -184,7 +186,7 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
                 CPG_HIP(launch_viterbi(vc, d_vt, buf_packed(b), nd, D, ws_vit, ctx->ws[WS_VIT].bytes,
                                        buf_out(b), d_score + start / D, nullptr, ctx->d_status,
                                        sdec));
-                CPG_HIP(launch_islands(buf_packed(b), buf_out(b), nd, D, start / D, ws_isl,
+                CPG_HIP(launch_islands(buf_packed(b), buf_out(b), nd, D, chunk0 + start / D, ws_isl,
                                        ctx->ws[WS_ISL].bytes, d_isl, island_cap, d_icnt + k + 1,
                                        sdec, d_icnt + k));
             } else {

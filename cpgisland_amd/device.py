@@ -136,15 +136,16 @@ def ingest(ctx: Context, d_txt: torch.Tensor, n: int, mode: int, compat_quirks: 
 def genome_run(ctx: Context, train_model: HmmModel | None, decode_model: HmmModel | None,
                packed: np.ndarray, sign: np.ndarray | None, nbases: int,
                window_bases: int = 0, nbuf: int = 0, want_sign_out: bool = True,
-               island_cap: int = 1 << 20):
+               island_cap: int = 1 << 20, first_chunk: int = 0):
     """Streamed whole-genome pass from HOST memory (cpg_genome_run, BASELINE config C5).
 
     Returns a dict: estep (105 doubles) | counts (124 int64) | sign_out (uint32 words) |
     scores (per decode chunk) | islands (records)."""
     assert packed.dtype == np.uint32 and packed.flags["C_CONTIGUOUS"]
-    opts = np.zeros(2, np.int64)
+    opts = np.zeros(3, np.int64)
     opts[0] = window_bases
     opts[1] = nbuf            # nbuf (int32) + reserved (int32), little endian
+    opts[2] = first_chunk
     est = np.zeros(_lib.COUNTS_F64_N, np.float64) if train_model is not None else None
     cnt = np.zeros(_lib.COUNTS_I64_N, np.int64) if sign is not None else None
     ndec = nbases // _lib.DECODE_CHUNK

@@ -268,6 +268,8 @@ typedef struct cpg_genome_opts {
     int64_t window_bases;   /* multiple of CPG_DECODE_CHUNK; 0: 64 Mi */
     int     nbuf;           /* device window buffers, 2..8; 0: 3 */
     int     reserved;
+    int64_t first_chunk;    /* decode-chunk index of base 0 (a shard of a larger genome):
+                               island coordinates / chunk numbers as in the unsharded run */
 } cpg_genome_opts;
 int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model, const cpg_model* decode_model,
                    const uint32_t* packed, const uint32_t* sign, int64_t nbases,

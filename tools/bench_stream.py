@@ -51,7 +51,7 @@ def main():
     cap = 1 << 22
     isl = np.zeros(cap, _lib.ISLAND_DTYPE)
     icount = C.c_int64()
-    opts = np.zeros(2, np.int64)
+    opts = np.zeros(3, np.int64)
     opts[0], opts[1] = args.window, args.nbuf
     lab = None if args.no_labels else sign
 
