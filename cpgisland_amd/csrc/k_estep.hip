@@ -353,6 +353,9 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
 #ifndef EST_ABL
 #define EST_ABL 0
 #endif
+#ifndef EST_PF
+#define EST_PF 0   // prefetch the backward pass's table rows one position ahead
+#endif
     unsigned long long sink = 0;   // ablations only
 #ifndef EST_MB_UNROLL
 #define EST_MB_UNROLL 1
@@ -392,8 +395,23 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         // since position 15, ef = alpha's shifts between positions p-1 and 14
         double rz0 = 0.0, rz = 0.0;
         int eb = 0, ef = 0;
+        // table rows of the next (lower) position are read one position ahead, before this
+        // position's LDS atomics: LDS operations retire in order, so a read issued after the
+        // atomics would make every position wait for the previous position's atomics
+#if EST_PF
+        double2 pma = TA[code_at(cm, kMB - 1)], pmb = TB[code_at(cm, kMB - 1)];
+#endif
 #pragma unroll
         for (int i = kMB - 1; i >= 0; --i) {
+#if EST_PF
+            const double2 cma = pma, cmb = pmb;
+            if (i > 0) {
+                pma = TA[code_at(cm, i - 1)];
+                pmb = TB[code_at(cm, i - 1)];
+            }
+#else
+            const double2 cma = TA[code_at(cm, i)], cmb = TB[code_at(cm, i)];
+#endif
             if (t == 0 && m == 0 && i == 0) {   // gamma_0 -> init counts
                 const double gp = alP[0] * yP, gm = alM[0] * yM, z = gp + gm;
                 g0P = gp / z;
@@ -405,8 +423,10 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             const uint32_t d = code_at(cm, i);
 #if EST_ABL == 3   // development ablation: no table reads in the backward pass
             const double2 ma = make_double2(0.5 + d * 1e-3, 0.25), mb = make_double2(0.125, 0.5);
+            (void)cma;
+            (void)cmb;
 #else
-            const double2 ma = TA[d], mb = TB[d];
+            const double2 ma = cma, mb = cmb;
 #endif
             // M beta products, shared by the pair marginals and the beta update
             const double t00 = ma.x * yP, t01 = ma.y * yM, t10 = mb.x * yP, t11 = mb.y * yM;
