@@ -122,7 +122,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--bases", type=int, default=N_PER_GPU, help="bases per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-sample", type=int, default=64 * DECODE)
+    ap.add_argument("--cpu-sample", type=int, default=192 * DECODE)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
     ap.add_argument("--prio", type=int, default=1,
