@@ -21,6 +21,9 @@ namespace {
 
 constexpr int kCountThreads = 256;
 constexpr int kRaw = 72;        // tot[16] pp[16] pm[16] mp[16] init[8]
+// workgroups add into kCntRep replicated accumulator sets (blockIdx % kCntRep) so that 1,024
+// workgroups do not serialise on 72 device-scope atomic addresses; the finalize sums them
+constexpr int kCntRep = 16;
 constexpr uint32_t M55 = 0x55555555u;
 
 struct Masks {
@@ -163,7 +166,8 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
         } else {
             acc = sinit[threadIdx.x - 64];
         }
-        if (acc) atomicAdd(gacc + threadIdx.x, (unsigned long long)acc);
+        if (acc) atomicAdd(gacc + (blockIdx.x % kCntRep) * kRaw + threadIdx.x,
+                           (unsigned long long)acc);
     }
 }
 
@@ -172,9 +176,13 @@ __global__ __launch_bounds__(128) void k_count_final(unsigned long long* __restr
                                                      int64_t* __restrict__ out) {
     __shared__ uint64_t raw[kRaw];
     const int t = threadIdx.x;
-    if (t < kRaw) raw[t] = gacc[t];
+    if (t < kRaw) {
+        uint64_t v = 0;
+        for (int r = 0; r < kCntRep; ++r) v += gacc[r * kRaw + t];
+        raw[t] = v;
+    }
     __syncthreads();
-    if (t < kRaw) gacc[t] = 0ull;
+    for (int i = t; i < kRaw * kCntRep; i += blockDim.x) gacc[i] = 0ull;
     if (t < 124) final_counts(raw, t, out);
 }
 
@@ -234,6 +242,6 @@ hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nc
     return hipGetLastError();
 }
 
-size_t count_ws_bytes(int64_t) { return (size_t)kRaw * 8; }
+size_t count_ws_bytes(int64_t) { return (size_t)kRaw * 8 * kCntRep; }
 
 }  // namespace cpg

@@ -33,6 +33,13 @@ namespace {
 constexpr int kET = 1024;               // max lanes per chunk
 constexpr int kLanePos = 64;            // positions per lane
 constexpr int kSlab = 73;               // trans[64] (by dinucleotide x 4) | init[8] | loglik
+// workgroups add into kAccRep replicated accumulator sets (chosen by chunk index) so that
+// ~700 workgroups do not serialise on 73 device-scope atomic addresses; the finalize sums
+// the replicas in 128-bit integer arithmetic (exact, order-independent)
+#ifndef EST_ACC_REP
+#define EST_ACC_REP 16
+#endif
+constexpr int kAccRep = EST_ACC_REP;
 // xi bins of one 16-lane replica: [k = from,to pair][d] (64 x u64) padded to 80 so that the
 // two replicas an LDS pass serves sit in opposite bank halves (80 * 8 B = 640 B = 160 banks)
 #ifndef EST_REP
@@ -472,21 +479,22 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     }
     __syncthreads();
     CPG_EST_MARK(T7)
+    unsigned long long* racc = acc + 2 * kSlab * (c % kAccRep);
     // chunk results -> the global 128-bit accumulators: xi bins and the init posteriors in
     // 2^-47 units, the log-likelihood in signed 2^-24 units
     if (t < 64) {   // row t = d * 4 + k
         unsigned long long s = 0;
         for (int q = 0; q < nw; ++q) s += part[q * 64 + t];
-        acc128_add(acc + 2 * t, s, false);
+        acc128_add(racc + 2 * t, s, false);
     }
     if (EST_ABL && sink == 0x123456789ull) acc[0] = sink;   // keep the ablated work live
     if (t == 0) {
-        acc128_add(acc + 2 * (64 + o0), to_fixed_scaled(g0P * kFix), false);
-        acc128_add(acc + 2 * (64 + o0 + 4), to_fixed_scaled(g0M * kFix), false);
+        acc128_add(racc + 2 * (64 + o0), to_fixed_scaled(g0P * kFix), false);
+        acc128_add(racc + 2 * (64 + o0 + 4), to_fixed_scaled(g0M * kFix), false);
     }
     if (t == nl - 1) {
         const long long L = llrint(ldexp(loglik, kLogFix));
-        acc128_add(acc + 2 * 72, (unsigned long long)L, L < 0);
+        acc128_add(racc + 2 * 72, (unsigned long long)L, L < 0);
     }
 #ifdef CPG_DEBUG_ESTEP
     if (t == 0 && (c == 0 || c == 300 || c == (int64_t)gridDim.x - 1))
@@ -505,7 +513,13 @@ __global__ __launch_bounds__(256) void k_estep_final(unsigned long long* __restr
     __shared__ double vsum[kSlab];
     const int t = threadIdx.x;
     if (t < kSlab) {
-        unsigned long long lo = acc[2 * t], hi = acc[2 * t + 1];
+        unsigned long long lo = 0ull, hi = 0ull;   // 128-bit sum of the replicas
+        for (int r = 0; r < kAccRep; ++r) {
+            const unsigned long long l = acc[2 * (r * kSlab + t)], h = acc[2 * (r * kSlab + t) + 1];
+            const unsigned long long nl = lo + l;
+            hi += h + (nl < lo ? 1ull : 0ull);
+            lo = nl;
+        }
         const bool neg = (long long)hi < 0;   // only the log-likelihood row can be negative
         if (neg) {                             // magnitude first: no cancellation
             lo = ~lo + 1ull;
@@ -515,7 +529,7 @@ __global__ __launch_bounds__(256) void k_estep_final(unsigned long long* __restr
         vsum[t] = t < 72 ? mag * (1.0 / kFix) : ldexp(neg ? -mag : mag, -kLogFix);
     }
     __syncthreads();
-    if (t < 2 * kSlab) acc[t] = 0ull;
+    for (int i = t; i < 2 * kSlab * kAccRep; i += blockDim.x) acc[i] = 0ull;
     if (t < 105) final_estep(vsum, t, out);
 }
 
@@ -545,7 +559,7 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
 
 }  // namespace
 
-size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8; }
+size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep; }
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t C, unsigned long long* acc, double* out, hipStream_t s,
