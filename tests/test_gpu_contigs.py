@@ -154,3 +154,34 @@ def test_contig_layout_violation_reported(gpu_ctx, torch_dev):
     torch.cuda.synchronize()
     with pytest.raises(CpgInvalid):
         gpu_ctx.sync()
+
+
+@pytest.mark.parametrize("kind", ["trained", "degenerate_pi"])
+def test_contig_viterbi_other_models(gpu_ctx, batch, kind):
+    """Trained model (one BW iteration) and a model with pi = 0 for some states: contigs whose
+    first base has pi = 0 for both live states decode as the reference does (all '+',
+    score -Double.MAX_VALUE propagated), the others exactly."""
+    import torch
+    from cpgisland_amd import HmmModel
+    from cpgisland_amd import device as D
+    m = co.initial_model()
+    if kind == "trained":
+        o = batch["obs"][: 8 * 65536]
+        m = co.normalize(co.estep(m, o, 65536))
+    else:
+        m = m.copy()
+        m[[0, 4]] = 0.0          # pi(A+) = pi(A-) = 0
+        m[:8] /= m[:8].sum()
+    d = batch["dev"]
+    n = len(batch["lens"])
+    so, sc = D.contigs_viterbi(gpu_ctx, HmmModel.from_struct(m), d["packed"], batch["span"],
+                               d["offs"], d["lens"], _order(gpu_ctx, batch, True), n)
+    torch.cuda.synchronize()
+    gpu_ctx.sync()
+    sg = D.sign_to_numpy(so, batch["span"] + 64)
+    sc = sc.cpu().numpy()
+    for c in range(n):
+        o, L = int(batch["offs"][c]), int(batch["lens"][c])
+        st, best = co.viterbi8(m, batch["obs"][o:o + L])
+        assert np.array_equal(sg[o:o + L], (st < 4).astype(np.uint8)), c
+        assert sc[c] == best or (best <= -1e308 and sc[c] <= -1e308), (c, sc[c], best)
