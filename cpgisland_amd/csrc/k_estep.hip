@@ -186,7 +186,8 @@ __device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int
 __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
                                                      const uint32_t* __restrict__ packed,
                                                      int64_t C,
-                                                     unsigned long long* __restrict__ acc) {
+                                                     unsigned long long* __restrict__ acc,
+                                                     const double2* __restrict__ gtab) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves
@@ -360,6 +361,13 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
 #ifndef EST_ABL
 #define EST_ABL 0
 #endif
+#ifndef EST_GTAB
+// 1: the backward pass reads its table rows from a global copy (L1-resident): those loads are
+// waited on with vmcnt, not lgkmcnt, so they do not wait for the preceding LDS atomics
+// (LDS operations retire in order); measured -5 %.  2: the forward recompute too (+20 %:
+// its chain then waits on the longer global latency).
+#define EST_GTAB 1
+#endif
 #ifndef EST_PF
 #define EST_PF 0   // prefetch the backward pass's table rows one position ahead
 #endif
@@ -388,7 +396,11 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
                 continue;
             }
             const uint32_t d = code_at(cm, i);
+#if EST_GTAB >= 2
+            const double2 ma = gtab[d], mb = gtab[16 + d];
+#else
             const double2 ma = TA[d], mb = TB[d];
+#endif
             const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
             xP = nP;
             xM = nM;
@@ -417,7 +429,11 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
                 pmb = TB[code_at(cm, i - 1)];
             }
 #else
+#if EST_GTAB   // the same rows from a global copy: waited on with vmcnt, not behind the atomics
+            const double2 cma = gtab[code_at(cm, i)], cmb = gtab[16 + code_at(cm, i)];
+#else
             const double2 cma = TA[code_at(cm, i)], cmb = TB[code_at(cm, i)];
+#endif
 #endif
             if (t == 0 && m == 0 && i == 0) {   // gamma_0 -> init counts
                 const double gp = alP[0] * yP, gm = alM[0] * yM, z = gp + gm;
@@ -504,6 +520,16 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
 #endif
 }
 
+// the 1-step tables of the model in global memory (rows TA | TB), for EST_GTAB
+__global__ void k_estep_tabs(const cpg_model model, double2* __restrict__ gtab) {
+    const int t = threadIdx.x;
+    if (t < 16) {
+        const int p = t & 3, b = t >> 2;
+        gtab[t] = make_double2(model.a[p][b], model.a[p][b + 4]);
+        gtab[16 + t] = make_double2(model.a[p + 4][b], model.a[p + 4][b + 4]);
+    }
+}
+
 __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 
 // One workgroup: the 73 accumulators -> doubles (re-zeroed for the next call), then the
@@ -559,7 +585,7 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
 
 }  // namespace
 
-size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep; }
+size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep + 1024; }
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t C, unsigned long long* acc, double* out, hipStream_t s,
@@ -572,8 +598,10 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
         const size_t uni = kUnionBytes;   // sized for 16 waves; fewer lanes use a prefix
         const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long) +
                            (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
+        double2* gtab = reinterpret_cast<double2*>(acc + 2 * kSlab * kAccRep);
+        if (EST_GTAB) hipLaunchKernelGGL(k_estep_tabs, dim3(1), dim3(64), 0, s, model, gtab);
         hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
-                           packed, C, acc);
+                           packed, C, acc, (const double2*)gtab);
     }
     if (parts & PART_FINAL)
         hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);
