@@ -244,6 +244,7 @@ def main():
         if flush is not None:
             flush.fill_(1.0)
         step(it)
+    issue = time.perf_counter() - t0   # host time to enqueue every step (launch-bound check)
     main_s.wait_stream(s_tr)
     main_s.wait_stream(s_dec)
     torch.cuda.synchronize()
@@ -304,6 +305,7 @@ def main():
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
                           "islands_found": int(icnt.item())},
                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
+               "host_issue_ms_per_step": round(issue * 1e3 / steps, 4),
                "roofline": roof, "roofline_decode": roof_decode}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(SEED, args.cpu_sample,

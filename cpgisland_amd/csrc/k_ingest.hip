@@ -11,7 +11,7 @@
 // training reader writes an extra all-A (zero-padded) chunk, the decode reader throws
 // (observedSequence.get(i) on an empty list).  Those bytes are the "quirk" bytes here.
 //
-// Per 16 KiB tile (one 256-lane workgroup, coalesced 16-B loads):
+// Per 32 KiB tile (one 256-lane workgroup, coalesced 16-B loads):
 //   * SWAR byte classification: fold case (x & 0xDF), code = ((f>>1)^(f>>2)) & 3 gives
 //     A,C,G,T -> 0,1,2,3, and a byte is valid iff f equals perm({A,C,G,T}, code)
 //     (v_perm_b32 as a 4-entry byte table);
@@ -42,8 +42,12 @@ namespace cpg {
 namespace {
 
 constexpr int kIT = 256;                       // lanes per tile
-constexpr int kIRows = 4;                      // rows of 1 KiB per wave
-constexpr int kTileBytes = kIT * 16 * kIRows;  // 16 KiB
+#ifndef ING_ROWS
+#define ING_ROWS 8
+#endif
+constexpr int kIRows = ING_ROWS;               // rows of 1 KiB per wave (8: 32 KiB tiles)
+constexpr int kTileBytes = kIT * 16 * kIRows;  // <= 32 KiB: one residue point per tile
+static_assert(kIRows % 2 == 0 && kTileBytes <= 32768, "2..8 rows of 1 KiB per wave");
 constexpr int kTileWords = kTileBytes / 16;    // packed words for a tile of valid bytes
 constexpr unsigned long long kFlagAgg = 1ull << 62, kFlagInc = 2ull << 62;
 constexpr unsigned long long kValMask = (1ull << 62) - 1;
@@ -191,7 +195,7 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
     uint32_t vm[kIRows], cw[kIRows], real[kIRows];
 #pragma unroll
     for (int r = 0; r < kIRows; ++r) {
-        const long long off = base + wv * 4096 + r * 1024 + lane * 16;
+        const long long off = base + wv * (kIRows * 1024) + r * 1024 + lane * 16;
         uint4 q = make_uint4(0u, 0u, 0u, 0u);
         real[r] = 0xFFFFu;
         if (off + 16 <= a.n) {
@@ -222,31 +226,34 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
         cw[r] = cnt[r] == 16 ? u : (u & ((1u << (2 * cnt[r])) - 1u));
     }
     // scans: two rows packed per 32-bit word (counts <= 1024 per row per wave)
-    uint32_t x01 = cnt[0] | (cnt[1] << 16), x23 = cnt[2] | (cnt[3] << 16);
+    uint32_t xs[kIRows / 2];
+#pragma unroll
+    for (int h = 0; h < kIRows / 2; ++h) xs[h] = cnt[2 * h] | (cnt[2 * h + 1] << 16);
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y01 = __shfl_up(x01, off), y23 = __shfl_up(x23, off);
-        if (lane >= off) {
-            x01 += y01;
-            x23 += y23;
+#pragma unroll
+        for (int h = 0; h < kIRows / 2; ++h) {
+            const uint32_t y = __shfl_up(xs[h], off);
+            if (lane >= off) xs[h] += y;
         }
     }
     if (lane == 63) {
-        srow[wv][0] = x01 & 0xFFFFu;
-        srow[wv][1] = x01 >> 16;
-        srow[wv][2] = x23 & 0xFFFFu;
-        srow[wv][3] = x23 >> 16;
+#pragma unroll
+        for (int h = 0; h < kIRows / 2; ++h) {
+            srow[wv][2 * h] = xs[h] & 0xFFFFu;
+            srow[wv][2 * h + 1] = xs[h] >> 16;
+        }
     }
     __syncthreads();
-    uint32_t o[kIRows] = {0u, 0u, 0u, 0u};   // tile-local index of the lane's first valid byte in each row
+    uint32_t o[kIRows];   // tile-local index of the lane's first valid byte in each row
     uint32_t agg = 0;
     {
         uint32_t before = 0;
         for (int w = 0; w < 4; ++w)
+#pragma unroll
             for (int r = 0; r < kIRows; ++r) {
                 if (w == wv) {
-                    const uint32_t incl = r == 0 ? (x01 & 0xFFFFu) : r == 1 ? (x01 >> 16)
-                                        : r == 2 ? (x23 & 0xFFFFu) : (x23 >> 16);
+                    const uint32_t incl = (r & 1) ? (xs[r >> 1] >> 16) : (xs[r >> 1] & 0xFFFFu);
                     o[r] = before + incl - cnt[r];
                 }
                 before += srow[w][r];
@@ -296,7 +303,7 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
                 if ((inv >> k) & 1u) {
                     if ((long long)before == ls) {
                         ++q;
-                        const long long kb = base + wv * 4096 + r * 1024 + lane * 16 + k;
+                        const long long kb = base + wv * (kIRows * 1024) + r * 1024 + lane * 16 + k;
                         kmin = kb < kmin ? kb : kmin;
                     }
                 } else if ((vm[r] >> k) & 1u) {
@@ -319,7 +326,7 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
             if (jw < o[r] || jw >= o[r] + cnt[r]) continue;
             uint32_t m = vm[r];
             for (uint32_t s = o[r]; s < jw; ++s) m &= m - 1;   // drop lower valid bytes
-            s_wrapk = base + wv * 4096 + r * 1024 + lane * 16 + (__builtin_ffs(m) - 1);
+            s_wrapk = base + wv * (kIRows * 1024) + r * 1024 + lane * 16 + (__builtin_ffs(m) - 1);
         }
     }
     __syncthreads();
