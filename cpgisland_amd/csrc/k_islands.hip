@@ -5,23 +5,35 @@
 //   start  = S & ~S_prev          (:319-337, inIsland false -> true)
 //   close  = ~S & S_prev          (:273-289, the '-' that ends the island; end = i-1)
 //   C, G   = base masks, CGm = G & C_prev (a G whose predecessor is a C)
-// Island counts are differences of per-word prefix sums; CpG inside (beg, end] is exact
-// from CGm.  The one serial quirk — `atC` is never cleared when an island closes (:325-331),
-// so the first pair of an island can count a CpG against the previous island's last C — is
-// a function stale_in -> stale_out per island (const 0 / const 1 / identity), resolved by a
-// scan over the chunk's islands.  Islands still open at the chunk end are dropped (:269-339
-// never closes them).  Coordinates and (cgCount*islandLen) use Java int arithmetic.
+// Island counts are differences of chunk-prefix counts taken at the run boundaries; CpG
+// inside (beg, end] is exact from CGm.  The one serial quirk — `atC` is never cleared when an
+// island closes (:325-331), so the first pair of an island can count a CpG against the
+// previous island's last C — is a function stale_in -> stale_out per island (const 0 /
+// const 1 / identity), resolved by a scan over the chunk's islands.  Islands still open at
+// the chunk end are dropped (:269-339 never closes them).  Coordinates and
+// (cgCount*islandLen) use Java int arithmetic.
 //
-// Kernels: A1 (per 1024-word tile) tile totals; A3 (per tile) word prefixes + run
-// boundaries, offset = sum of earlier tiles; B (per chunk) per-run stats, stale scan, filter,
-// kept rank; D (per chunk) records at offset = kept islands of earlier chunks.
+// Kernels:
+//   T (per tile of 4,096 words = 131,072 positions, all CUs streaming): counts, a workgroup
+//     scan, and a record per run boundary with the tile-local prefix counts at it, written
+//     at its tile-local rank into the tile's slice of the run lists; the tile totals;
+//   R (per chunk): tile offsets (scan of the tile totals), per-run stats, stale-atC scan,
+//     filter, kept rank;
+//   D (per chunk): island records at offset = kept islands of earlier chunks.
+// A whole chunk per workgroup would stream at one CU's share of the memory system (≈25-70
+// GB/s per CU): the tiles spread the one pass over the data on every CU.
+
+#include <algorithm>
 
 #include "cpg_internal.h"
 
 namespace cpg {
 namespace {
 
-constexpr int kIT = 1024;
+constexpr int kIT = 1024;    // lanes of the per-chunk kernels
+constexpr int kTT = 256;     // lanes of the tile kernel
+constexpr int kTRows = 4;    // rows of kTT * 4 words per tile
+constexpr int64_t kTW = (int64_t)kTT * 4 * kTRows;   // words per tile (4,096)
 
 __device__ __forceinline__ uint32_t compact16(uint32_t x) {   // even bits -> low 16 bits
     x &= 0x55555555u;
@@ -54,104 +66,9 @@ __device__ __forceinline__ WordMasks masks_reg(uint32_t S, uint32_t Sprev, uint3
     return m;
 }
 
-// the 4 sign words a lane owns (w0..w0+3), all loads vectorised; words >= nw read as 0
-__device__ __forceinline__ void masks4(const uint32_t* __restrict__ pk,
-                                       const uint32_t* __restrict__ sg, int64_t w0, int64_t nw,
-                                       WordMasks (&m)[4]) {
-    uint32_t S[4], P[8], sprev, pprev;
-    if (w0 + 4 <= nw) {
-        const uint4 s4 = *reinterpret_cast<const uint4*>(sg + w0);
-        const uint4 p0 = *reinterpret_cast<const uint4*>(pk + 2 * w0);
-        const uint4 p1 = *reinterpret_cast<const uint4*>(pk + 2 * w0 + 4);
-        S[0] = s4.x; S[1] = s4.y; S[2] = s4.z; S[3] = s4.w;
-        P[0] = p0.x; P[1] = p0.y; P[2] = p0.z; P[3] = p0.w;
-        P[4] = p1.x; P[5] = p1.y; P[6] = p1.z; P[7] = p1.w;
-    } else {
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const bool in = w0 + i < nw;
-            S[i] = in ? sg[w0 + i] : 0u;
-            P[2 * i] = in ? pk[2 * (w0 + i)] : 0u;
-            P[2 * i + 1] = in ? pk[2 * (w0 + i) + 1] : 0u;
-        }
-    }
-    sprev = w0 > 0 ? sg[w0 - 1] : 0u;
-    pprev = w0 > 0 ? pk[2 * w0 - 1] : 0u;
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-        m[i] = masks_reg(S[i], i == 0 ? sprev : S[i - 1], P[2 * i], P[2 * i + 1],
-                         i == 0 ? pprev : P[2 * i - 1]);
-}
-
-// masks of sign word w (positions 32w..32w+31) of a chunk; nw = words in the chunk
-__device__ __forceinline__ WordMasks word_masks(const uint32_t* __restrict__ pk,
-                                                const uint32_t* __restrict__ sg, int64_t w) {
-    WordMasks m;
-    const uint32_t S = sg[w];
-    const uint32_t sprev = w > 0 ? (sg[w - 1] >> 31) : 0u;
-    const uint32_t Sp = (S << 1) | sprev;
-    m.S = S;
-    m.start = S & ~Sp;
-    m.close = ~S & Sp;
-    const uint32_t w0 = pk[2 * w], w1 = pk[2 * w + 1];
-    const uint32_t h0 = w0 >> 1, h1 = w1 >> 1;
-    const uint32_t c = compact16(w0 & ~h0) | (compact16(w1 & ~h1) << 16);   // base == 1
-    const uint32_t g = compact16(h0 & ~w0) | (compact16(h1 & ~w1) << 16);   // base == 2
-    const uint32_t cprev = w > 0 ? ((pk[2 * w - 1] >> 30) == 1u) : 0u;
-    m.C = c;
-    m.G = g;
-    m.CG = g & ((c << 1) | cprev);
-    return m;
-}
-
 struct Cnt5 {
     int32_t c, g, cg, st, cl;
 };
-
-struct IslWs {
-    int32_t* Cp;        // per word exclusive prefix (chunk-local)
-    int32_t* Gp;
-    int32_t* CGp;
-    uint32_t* starts;   // per run
-    uint32_t* closes;
-    int32_t* kept;      // per run: rank*2 | stale_in, or -1
-    int32_t* nruns;     // per chunk
-    int32_t* ncloses;
-    int64_t* nkept;
-    void* tiles;        // Cnt5 per (chunk, tile)
-    size_t bytes;
-};
-
-IslWs carve_isl(void* base, int64_t nchunks, int64_t C) {
-    const int64_t nw = (C + 31) / 32, maxr = C / 2 + 1;
-    char* p = static_cast<char*>(base);
-    size_t o = 0;
-    auto take = [&](size_t b) {
-        o = (o + 255) & ~size_t(255);
-        char* r = p ? p + o : nullptr;
-        o += b;
-        return r;
-    };
-    IslWs w;
-    w.Cp = (int32_t*)take(nchunks * nw * 4);
-    w.Gp = (int32_t*)take(nchunks * nw * 4);
-    w.CGp = (int32_t*)take(nchunks * nw * 4);
-    w.starts = (uint32_t*)take(nchunks * maxr * 4);
-    w.closes = (uint32_t*)take(nchunks * maxr * 4);
-    w.kept = (int32_t*)take(nchunks * maxr * 4);
-    w.nruns = (int32_t*)take(nchunks * 4);
-    w.ncloses = (int32_t*)take(nchunks * 4);
-    w.nkept = (int64_t*)take(nchunks * 8);
-    w.tiles = take(nchunks * ((nw + 1023) / 1024) * 20 + 16);
-    w.bytes = o + 256;
-    return w;
-}
-
-
-// Pass A, tiled: a tile = 1024 sign words (32,768 positions) of one chunk, 4 words per lane.
-constexpr int kTileW = 1024;
-constexpr int kAT = 256;
-
 __device__ __forceinline__ Cnt5 cnt_of(const WordMasks& m) {
     return Cnt5{(int32_t)__popc(m.C), (int32_t)__popc(m.G), (int32_t)__popc(m.CG),
                 (int32_t)__popc(m.start), (int32_t)__popc(m.close)};
@@ -161,127 +78,254 @@ __device__ __forceinline__ Cnt5 cadd(Cnt5 a, const Cnt5& b) {
     return a;
 }
 
-// block-wide exclusive scan of one Cnt5 per lane; returns (exclusive, total)
-__device__ __forceinline__ Cnt5 block_scan(Cnt5 v, Cnt5* sb, Cnt5& total) {
-    const int t = threadIdx.x;
-    sb[t] = v;
-    __syncthreads();
-    for (int off = 1; off < kAT; off <<= 1) {
-        Cnt5 x = sb[t];
-        if (t >= off) x = cadd(x, sb[t - off]);
-        __syncthreads();
-        sb[t] = x;
-        __syncthreads();
-    }
-    total = sb[kAT - 1];
-    const Cnt5 e = t > 0 ? sb[t - 1] : Cnt5{0, 0, 0, 0, 0};
-    __syncthreads();
-    return e;
+// a run boundary with the prefix counts at it: start records carry C, G before `pos` and
+// CpG up to and including `pos` (the run's first pair is (pos, pos+1)); close records carry
+// C, G, CpG before `pos` (the first '-' after the run).  `pos` is chunk-relative; the counts
+// are tile-relative in the lists (the tile offsets are added when a record is read).
+struct RunRec {
+    uint32_t pos;
+    int32_t c, g, cg;
+};
+
+struct IslWs {
+    RunRec* starts;     // per tile, cap_t records
+    RunRec* closes;
+    Cnt5* ttot;         // per tile: totals (kernel T)
+    Cnt5* toff;         // per tile: exclusive prefix in its chunk (kernel R)
+    int32_t* kept;      // per chunk, maxr: rank*2 | stale_in, or -1
+    int32_t* ncloses;   // per chunk
+    int64_t* nkept;
+    int64_t ntile;      // tiles per chunk
+    int64_t cap_t;      // records per tile and kind
+    size_t bytes;
+};
+
+IslWs carve_isl(void* base, int64_t nchunks, int64_t C) {
+    const int64_t nw = C / 32, maxr = C / 2 + 1;
+    IslWs w;
+    w.ntile = std::max<int64_t>(1, (nw + kTW - 1) / kTW);
+    w.cap_t = std::min<int64_t>(kTW * 16 + 1, maxr);   // a tile holds <= 16 runs per word
+    char* p = static_cast<char*>(base);
+    size_t o = 0;
+    auto take = [&](size_t b) {
+        o = (o + 255) & ~size_t(255);
+        char* r = p ? p + o : nullptr;
+        o += b;
+        return r;
+    };
+    const int64_t nt = nchunks * w.ntile;
+    w.starts = (RunRec*)take(nt * w.cap_t * sizeof(RunRec));
+    w.closes = (RunRec*)take(nt * w.cap_t * sizeof(RunRec));
+    w.ttot = (Cnt5*)take(nt * sizeof(Cnt5));
+    w.toff = (Cnt5*)take(nt * sizeof(Cnt5));
+    w.kept = (int32_t*)take(nchunks * maxr * 4);
+    w.ncloses = (int32_t*)take(nchunks * 4);
+    w.nkept = (int64_t*)take(nchunks * 8);
+    w.bytes = o + 256;
+    return w;
 }
 
-// A1: tile totals
-__global__ __launch_bounds__(kAT) void k_isl_a1(const uint32_t* packed, const uint32_t* sign,
-                                               int64_t C, int ntiles, Cnt5* __restrict__ tiles) {
-    const int64_t c = blockIdx.x / ntiles;
-    const int tile = blockIdx.x - (int)c * ntiles;
+// the run boundaries of word w as records; e = the prefix counts before the word (advanced)
+__device__ __forceinline__ void emit_word(const WordMasks& q, int64_t w, Cnt5& e,
+                                          RunRec* __restrict__ st, RunRec* __restrict__ cl) {
+    for (uint32_t x = q.start; x; x &= x - 1) {
+        const int b = __ffs(x) - 1;
+        const uint32_t lo = (1u << b) - 1u;
+        st[e.st++] = RunRec{(uint32_t)(w * 32 + b), e.c + (int32_t)__popc(q.C & lo),
+                            e.g + (int32_t)__popc(q.G & lo),
+                            e.cg + (int32_t)__popc(q.CG & (lo | (1u << b)))};
+    }
+    for (uint32_t x = q.close; x; x &= x - 1) {
+        const int b = __ffs(x) - 1;
+        const uint32_t lo = (1u << b) - 1u;
+        cl[e.cl++] = RunRec{(uint32_t)(w * 32 + b), e.c + (int32_t)__popc(q.C & lo),
+                            e.g + (int32_t)__popc(q.G & lo), e.cg + (int32_t)__popc(q.CG & lo)};
+    }
+    e.c += __popc(q.C);
+    e.g += __popc(q.G);
+    e.cg += __popc(q.CG);
+}
+
+// the 4 words w0..w0+3 of a chunk (words >= nw read as 0) and the words before them
+struct Quad {
+    uint32_t S[4], P[8], sprev, pprev;
+};
+__device__ __forceinline__ Quad load_quad(const uint32_t* __restrict__ pk,
+                                          const uint32_t* __restrict__ sg, int64_t w0,
+                                          int64_t nw) {
+    Quad q;
+    if (w0 + 4 <= nw) {
+        const uint4 s4 = *reinterpret_cast<const uint4*>(sg + w0);
+        const uint4 p0 = *reinterpret_cast<const uint4*>(pk + 2 * w0);
+        const uint4 p1 = *reinterpret_cast<const uint4*>(pk + 2 * w0 + 4);
+        q.S[0] = s4.x; q.S[1] = s4.y; q.S[2] = s4.z; q.S[3] = s4.w;
+        q.P[0] = p0.x; q.P[1] = p0.y; q.P[2] = p0.z; q.P[3] = p0.w;
+        q.P[4] = p1.x; q.P[5] = p1.y; q.P[6] = p1.z; q.P[7] = p1.w;
+    } else {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const bool in = w0 + i < nw;
+            q.S[i] = in ? sg[w0 + i] : 0u;
+            q.P[2 * i] = in ? pk[2 * (w0 + i)] : 0u;
+            q.P[2 * i + 1] = in ? pk[2 * (w0 + i) + 1] : 0u;
+        }
+    }
+    q.sprev = (w0 > 0 && w0 < nw) ? sg[w0 - 1] : 0u;
+    q.pprev = (w0 > 0 && w0 < nw) ? pk[2 * w0 - 1] : 0u;
+    return q;
+}
+__device__ __forceinline__ WordMasks quad_masks(const Quad& q, int i) {   // i compile-time
+    return masks_reg(q.S[i], i ? q.S[i - 1] : q.sprev, q.P[2 * i], q.P[2 * i + 1],
+                     i ? q.P[2 * i - 1] : q.pprev);
+}
+
+// T: one tile.  Lane t owns words 4t..4t+3 of each of the tile's 4 rows of 1,024 words
+// (coalesced 16-B loads); the scan runs over (row, lane) in word order: the lane's four row
+// counts are packed two fields per 32-bit word (a wave row sums to <= 8,192) and scanned by
+// wave shuffles together, the wave totals of every row meet in LDS behind one barrier.
+__global__ __launch_bounds__(kTT) void k_isl_tile(const uint32_t* packed, const uint32_t* sign,
+                                                 int64_t C, IslWs ws) {
+    const int64_t c = blockIdx.x / ws.ntile;
+    const int64_t k = blockIdx.x - c * ws.ntile;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t nw = C / 32;
     const uint32_t* pk = packed + c * (C / 16);
     const uint32_t* sg = sign + c * nw;
-    Cnt5 s{0, 0, 0, 0, 0};
-    const int64_t w0 = (int64_t)tile * kTileW + threadIdx.x * 4;
-    WordMasks m[4];
-    if (w0 < nw) masks4(pk, sg, w0, nw, m);
+    Quad q[kTRows];
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (w0 + i < nw) s = cadd(s, cnt_of(m[i]));
-    __shared__ Cnt5 sb[kAT];
-    Cnt5 tot;
-    block_scan(s, sb, tot);
-    if (threadIdx.x == 0) tiles[blockIdx.x] = tot;
+    for (int r = 0; r < kTRows; ++r) q[r] = load_quad(pk, sg, k * kTW + r * (kTT * 4) + 4 * t, nw);
+    uint32_t x[kTRows][3], own[kTRows][3];
+#pragma unroll
+    for (int r = 0; r < kTRows; ++r) {
+        Cnt5 s{0, 0, 0, 0, 0};
+        const int64_t w0 = k * kTW + r * (kTT * 4) + 4 * t;
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+            if (w0 + i < nw) s = cadd(s, cnt_of(quad_masks(q[r], i)));
+        own[r][0] = x[r][0] = (uint32_t)s.c | ((uint32_t)s.g << 16);
+        own[r][1] = x[r][1] = (uint32_t)s.cg | ((uint32_t)s.st << 16);
+        own[r][2] = x[r][2] = (uint32_t)s.cl;
+    }
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+        for (int r = 0; r < kTRows; ++r)
+#pragma unroll
+            for (int f = 0; f < 3; ++f) {
+                const uint32_t y = __shfl_up(x[r][f], off);
+                if (lane >= off) x[r][f] += y;
+            }
+    }
+    __shared__ Cnt5 wt[kTRows][kTT / 64];
+    if (lane == 63)
+#pragma unroll
+        for (int r = 0; r < kTRows; ++r)
+            wt[r][wv] = Cnt5{(int32_t)(x[r][0] & 0xFFFFu), (int32_t)(x[r][0] >> 16),
+                             (int32_t)(x[r][1] & 0xFFFFu), (int32_t)(x[r][1] >> 16),
+                             (int32_t)x[r][2]};
+    __syncthreads();
+    RunRec* st = ws.starts + blockIdx.x * ws.cap_t;
+    RunRec* cl = ws.closes + blockIdx.x * ws.cap_t;
+    Cnt5 rowbase{0, 0, 0, 0, 0};
+#pragma unroll
+    for (int r = 0; r < kTRows; ++r) {
+        Cnt5 e = rowbase;
+#pragma unroll
+        for (int w = 0; w < kTT / 64; ++w) {
+            const Cnt5 s = wt[r][w];
+            if (w < wv) e = cadd(e, s);
+            rowbase = cadd(rowbase, s);
+        }
+        const uint32_t ex0 = x[r][0] - own[r][0], ex1 = x[r][1] - own[r][1], ex2 = x[r][2] - own[r][2];
+        e = cadd(e, Cnt5{(int32_t)(ex0 & 0xFFFFu), (int32_t)(ex0 >> 16), (int32_t)(ex1 & 0xFFFFu),
+                         (int32_t)(ex1 >> 16), (int32_t)ex2});
+        if ((own[r][1] >> 16) | own[r][2]) {   // the lane's words hold a run boundary
+            const int64_t w0 = k * kTW + r * (kTT * 4) + 4 * t;
+#pragma unroll
+            for (int i = 0; i < 4; ++i)
+                if (w0 + i < nw) emit_word(quad_masks(q[r], i), w0 + i, e, st, cl);
+        }
+    }
+    if (t == 0) ws.ttot[blockIdx.x] = rowbase;
 }
 
-// A3: word prefixes and run boundaries
-__global__ __launch_bounds__(kAT) void k_isl_a3(const uint32_t* packed, const uint32_t* sign,
-                                               int64_t C, int ntiles,
-                                               const Cnt5* __restrict__ tiles, IslWs ws) {
-    const int64_t c = blockIdx.x / ntiles;
-    const int tile = blockIdx.x - (int)c * ntiles;
-    const int64_t nw = C / 32, maxr = C / 2 + 1;
-    const uint32_t* pk = packed + c * (C / 16);
-    const uint32_t* sg = sign + c * nw;
-    const int64_t w0 = (int64_t)tile * kTileW + threadIdx.x * 4;
-    WordMasks m[4];
-    Cnt5 s{0, 0, 0, 0, 0};
-    if (w0 < nw) masks4(pk, sg, w0, nw, m);
+// workgroup scans (blockDim.x a multiple of 64, <= 1024): wave shuffles, the wave totals
+// through LDS, one barrier each.  Every call uses its own LDS array (no reuse barrier).
+__device__ __forceinline__ Cnt5 wg_scan5(const Cnt5 v, Cnt5* sw, Cnt5& total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    Cnt5 x = v;
 #pragma unroll
-    for (int i = 0; i < 4; ++i)
-        if (w0 + i < nw) s = cadd(s, cnt_of(m[i]));
-    __shared__ Cnt5 sb[kAT];
-    // this tile's offset in the chunk: the sum of the earlier tiles' A1 totals
-    Cnt5 before{0, 0, 0, 0, 0}, off, tot;
-    for (int i = threadIdx.x; i < tile; i += kAT) before = cadd(before, tiles[c * ntiles + i]);
-    block_scan(before, sb, off);
-    Cnt5 e = cadd(block_scan(s, sb, tot), off);
-    if (tile == ntiles - 1 && threadIdx.x == 0) {   // chunk totals: runs opened / closed
-        ws.nruns[c] = off.st + tot.st;
-        ws.ncloses[c] = off.cl + tot.cl;
+    for (int off = 1; off < 64; off <<= 1) {
+        const Cnt5 y{__shfl_up(x.c, off), __shfl_up(x.g, off), __shfl_up(x.cg, off),
+                     __shfl_up(x.st, off), __shfl_up(x.cl, off)};
+        if (lane >= off) x = cadd(x, y);
     }
-    int32_t* Cp = ws.Cp + c * nw;
-    int32_t* Gp = ws.Gp + c * nw;
-    int32_t* CGp = ws.CGp + c * nw;
-    uint32_t* st = ws.starts + c * maxr;
-    uint32_t* cl = ws.closes + c * maxr;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-        const int64_t w = w0 + i;
-        if (w >= nw) break;
-        Cp[w] = e.c;
-        Gp[w] = e.g;
-        CGp[w] = e.cg;
-        e.c += __popc(m[i].C);
-        e.g += __popc(m[i].G);
-        e.cg += __popc(m[i].CG);
-        for (uint32_t x = m[i].start; x; x &= x - 1) st[e.st++] = (uint32_t)(w * 32 + __ffs(x) - 1);
-        for (uint32_t x = m[i].close; x; x &= x - 1) cl[e.cl++] = (uint32_t)(w * 32 + __ffs(x) - 1);
+    if (lane == 63) sw[wv] = x;
+    __syncthreads();
+    Cnt5 before{0, 0, 0, 0, 0}, tot{0, 0, 0, 0, 0};
+    for (int w = 0; w < nwv; ++w) {
+        const Cnt5 s = sw[w];
+        if (w < wv) before = cadd(before, s);
+        tot = cadd(tot, s);
     }
+    total = tot;
+    return Cnt5{before.c + x.c - v.c, before.g + x.g - v.g, before.cg + x.cg - v.cg,
+                before.st + x.st - v.st, before.cl + x.cl - v.cl};
 }
 
 __device__ __forceinline__ uint32_t isl_base(const uint32_t* pk, int64_t pos) {
     return (pk[pos >> 4] >> ((pos & 15) * 2)) & 3u;
 }
-// prefix count of a mask kind (0 C, 1 G, 2 CG) over chunk positions [0, pos)
-__device__ __forceinline__ int32_t pref(const uint32_t* pk, const uint32_t* sg, const int32_t* P,
-                                        int kind, int64_t pos, int64_t nw) {
-    const int64_t w = pos >> 5;
-    if (w >= nw) return P[nw - 1] + __popc(kind == 0 ? word_masks(pk, sg, nw - 1).C
-                                           : kind == 1 ? word_masks(pk, sg, nw - 1).G
-                                                       : word_masks(pk, sg, nw - 1).CG);
-    const WordMasks m = word_masks(pk, sg, w);
-    const uint32_t x = kind == 0 ? m.C : kind == 1 ? m.G : m.CG;
-    const uint32_t lowmask = (pos & 31) ? ((1u << (pos & 31)) - 1u) : 0u;
-    return P[w] + __popc(x & lowmask);
+
+// a chunk's tile offsets: in LDS, or in global memory written by this same kernel (read
+// past this CU's L1: agent scope), or written by an earlier kernel (plain loads)
+template <bool kAgent>
+__device__ __forceinline__ int32_t ld_off(const int32_t* p) {
+    if constexpr (kAgent) return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    else return *p;
+}
+
+// the chunk's r-th start (kind 0) or close (kind 1) record with chunk-relative counts: the
+// last tile whose exclusive offset is <= r (binary search over the chunk's tile offsets `to`)
+template <bool kAgent>
+__device__ __forceinline__ RunRec run_rec(const IslWs& ws, const Cnt5* to, int64_t c, int64_t r,
+                                          int kind) {
+    int64_t lo = 0, hi = ws.ntile - 1;
+    while (lo < hi) {
+        const int64_t mid = (lo + hi + 1) >> 1;
+        const int32_t v = ld_off<kAgent>(kind ? &to[mid].cl : &to[mid].st);
+        if (v <= r) lo = mid; else hi = mid - 1;
+    }
+    const int32_t oc = ld_off<kAgent>(&to[lo].c), og = ld_off<kAgent>(&to[lo].g),
+                  ocg = ld_off<kAgent>(&to[lo].cg),
+                  ok = ld_off<kAgent>(kind ? &to[lo].cl : &to[lo].st);
+    const int64_t tile = c * ws.ntile + lo;
+    RunRec x = (kind ? ws.closes : ws.starts)[tile * ws.cap_t + (r - ok)];
+    x.c += oc;
+    x.g += og;
+    x.cg += ocg;
+    return x;
 }
 
 struct RunStat {
     int32_t beg, end, len, C, G, CGin;
     uint32_t b0, b1, last;
 };
-__device__ __forceinline__ RunStat run_stat(const uint32_t* pk, const uint32_t* sg, IslWs ws,
-                                            int64_t c, int64_t nw, uint32_t beg, uint32_t close) {
-    RunStat r;
-    r.beg = (int32_t)beg;
-    r.end = (int32_t)close - 1;
-    r.len = (int32_t)(close - beg);
-    const int32_t* Cp = ws.Cp + c * nw;
-    const int32_t* Gp = ws.Gp + c * nw;
-    const int32_t* CGp = ws.CGp + c * nw;
-    r.C = pref(pk, sg, Cp, 0, close, nw) - pref(pk, sg, Cp, 0, beg, nw);
-    r.G = pref(pk, sg, Gp, 1, close, nw) - pref(pk, sg, Gp, 1, beg, nw);
-    r.CGin = r.len >= 2 ? pref(pk, sg, CGp, 2, close, nw) - pref(pk, sg, CGp, 2, beg + 1, nw) : 0;
-    r.b0 = isl_base(pk, beg);
-    r.b1 = r.len >= 2 ? isl_base(pk, beg + 1) : 0u;
-    r.last = isl_base(pk, close - 1);
-    return r;
+template <bool kAgent>
+__device__ __forceinline__ RunStat run_stat(const uint32_t* pk, const IslWs& ws, const Cnt5* to,
+                                            int64_t c, int64_t r) {
+    const RunRec s = run_rec<kAgent>(ws, to, c, r, 0), e = run_rec<kAgent>(ws, to, c, r, 1);
+    RunStat o;
+    o.beg = (int32_t)s.pos;
+    o.end = (int32_t)e.pos - 1;
+    o.len = (int32_t)(e.pos - s.pos);
+    o.C = e.c - s.c;
+    o.G = e.g - s.g;
+    o.CGin = o.len >= 2 ? e.cg - s.cg : 0;
+    o.b0 = isl_base(pk, s.pos);
+    o.b1 = o.len >= 2 ? isl_base(pk, s.pos + 1) : 0u;
+    o.last = isl_base(pk, e.pos - 1);
+    return o;
 }
 // stale atC map (bit x = output for input x): const0 0b00, const1 0b11, id 0b10
 __device__ __forceinline__ uint32_t stale_map(const RunStat& r) {
@@ -312,64 +356,140 @@ __device__ __forceinline__ Rec filter(const RunStat& r, uint32_t stale_in) {
     return o;
 }
 
-__global__ __launch_bounds__(kIT) void k_isl_b(const uint32_t* packed, const uint32_t* sign,
-                                               int64_t C, IslWs ws) {
-    const int64_t c = blockIdx.x;
-    const int t = threadIdx.x;
-    const int64_t nw = C / 32, maxr = C / 2 + 1;
-    const uint32_t* pk = packed + c * (C / 16);
-    const uint32_t* sg = sign + c * nw;
-    const int64_t nr = ws.ncloses[c];   // closed runs only; an open last run is dropped
-    const uint32_t* st = ws.starts + c * maxr;
-    const uint32_t* cl = ws.closes + c * maxr;
-    int32_t* kept = ws.kept + c * maxr;
-    const int64_t per = (nr + kIT - 1) / kIT;
-    const int64_t r0 = min((int64_t)t * per, nr), r1 = min(r0 + per, nr);
-    uint32_t F = 0x2u;
-    for (int64_t r = r0; r < r1; ++r) F = mcompose(stale_map(run_stat(pk, sg, ws, c, nw, st[r], cl[r])), F);
-    __shared__ uint32_t sF[kIT];
-    __shared__ int32_t sK[kIT];
-    sF[t] = F;
+// exclusive composition scan of stale maps (lane order = run order)
+__device__ __forceinline__ uint32_t wg_scan_map(const uint32_t f, uint32_t* sw) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    uint32_t x = f;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(x, off);
+        if (lane >= off) x = mcompose(x, y);
+    }
+    if (lane == 63) sw[wv] = x;
     __syncthreads();
-    for (int off = 1; off < kIT; off <<= 1) {
-        uint32_t x = sF[t];
-        if (t >= off) x = mcompose(x, sF[t - off]);
-        __syncthreads();
-        sF[t] = x;
-        __syncthreads();
+    uint32_t before = 0x2u;   // identity
+    for (int w = 0; w < wv; ++w) before = mcompose(sw[w], before);
+    const uint32_t up = __shfl_up(x, 1);
+    return lane > 0 ? mcompose(up, before) : before;
+}
+__device__ __forceinline__ int32_t wg_scan_sum(const int32_t v, int32_t* sw, int32_t& total) {
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6, nwv = blockDim.x >> 6;
+    int32_t x = v;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const int32_t y = __shfl_up(x, off);
+        if (lane >= off) x += y;
     }
-    uint32_t stale = t > 0 ? mapply(sF[t - 1], 0u) : 0u;   // atC = false at chunk start (:268)
-    int32_t nk = 0;
-    for (int64_t r = r0; r < r1; ++r) {
-        const RunStat rs = run_stat(pk, sg, ws, c, nw, st[r], cl[r]);
-        const Rec o = filter(rs, stale);
-        kept[r] = o.keep ? (int32_t)(stale) : -1;   // rank added below
-#ifdef CPG_DEBUG_ISL
-        if (c == 0 && r < 8)
-            printf("run %d beg %d end %d len %d C %d G %d CGin %d b0 %u b1 %u last %u cg %f oe %f keep %d\n",
-                   (int)r, rs.beg, rs.end, rs.len, rs.C, rs.G, rs.CGin, rs.b0, rs.b1, rs.last, o.cg, o.oe, (int)o.keep);
-#endif
-        nk += o.keep;
-        stale = mapply(stale_map(rs), stale);
-    }
-    sK[t] = nk;
+    if (lane == 63) sw[wv] = x;
     __syncthreads();
-    for (int off = 1; off < kIT; off <<= 1) {
-        int32_t x = sK[t];
-        if (t >= off) x += sK[t - off];
-        __syncthreads();
-        sK[t] = x;
-        __syncthreads();
+    int32_t before = 0, tot = 0;
+    for (int w = 0; w < nwv; ++w) {
+        const int32_t s = sw[w];
+        before += w < wv ? s : 0;
+        tot += s;
     }
-    int32_t rank = t > 0 ? sK[t - 1] : 0;
-    for (int64_t r = r0; r < r1; ++r)
-        if (kept[r] >= 0) kept[r] |= (rank++) << 1;
-    if (t == kIT - 1) ws.nkept[c] = sK[kIT - 1];
+    total = tot;
+    return before + x - v;
 }
 
-__global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, const uint32_t* sign,
-                                               int64_t C, int64_t first_chunk, IslWs ws,
-                                               cpg_island* out, int64_t cap, int64_t* count,
+// the chunk's closed runs split over the lanes: stale-atC maps composed and scanned,
+// filtered (:280-285), kept islands ranked.  With <= 8 runs per lane the map and both filter
+// outcomes (stale 0 / 1) of each run stay in registers: one pass of loads.
+template <bool kAgent>
+__device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws, const Cnt5* to,
+                                             int64_t c, int64_t nr, int32_t* kept, uint32_t* sm,
+                                             int32_t* sk) {
+    const int t = threadIdx.x, nl = blockDim.x;
+    const int64_t per = (nr + nl - 1) / nl;
+    const int64_t r0 = min((int64_t)t * per, nr), r1 = min(r0 + per, nr);
+    constexpr int kCache = 8;
+    const bool cached = per <= kCache;   // uniform
+    uint32_t bits = 0;   // run j: bits 4j.. = map | keep(stale 0) << 2 | keep(stale 1) << 3
+    uint32_t F = 0x2u;
+    for (int64_t r = r0; r < r1; ++r) {
+        const RunStat rs = run_stat<kAgent>(pk, ws, to, c, r);
+        const uint32_t m = stale_map(rs);
+        F = mcompose(m, F);
+        if (cached)
+            bits |= (m | ((uint32_t)filter(rs, 0u).keep << 2) | ((uint32_t)filter(rs, 1u).keep << 3))
+                    << (4 * (r - r0));
+    }
+    const uint32_t stale0 = mapply(wg_scan_map(F, sm), 0u);   // atC = false at the chunk start (:268)
+    uint32_t stale = stale0;
+    int32_t nk = 0;
+    if (cached) {
+        for (int64_t j = 0; j < r1 - r0; ++j) {
+            const uint32_t b = bits >> (4 * j);
+            nk += (b >> (2 + stale)) & 1u;
+            stale = mapply(b & 3u, stale);
+        }
+    } else {
+        for (int64_t r = r0; r < r1; ++r) {
+            const RunStat rs = run_stat<kAgent>(pk, ws, to, c, r);
+            const Rec o = filter(rs, stale);
+            kept[r] = o.keep ? (int32_t)stale : -1;   // rank added below
+            nk += o.keep;
+            stale = mapply(stale_map(rs), stale);
+        }
+    }
+    int32_t nkt;
+    int32_t rank = wg_scan_sum(nk, sk, nkt);
+    if (cached) {
+        stale = stale0;
+        for (int64_t j = 0; j < r1 - r0; ++j) {
+            const uint32_t b = bits >> (4 * j);
+            kept[r0 + j] = ((b >> (2 + stale)) & 1u) ? (int32_t)(((uint32_t)rank++ << 1) | stale) : -1;
+            stale = mapply(b & 3u, stale);
+        }
+    } else {
+        for (int64_t r = r0; r < r1; ++r)
+            if (kept[r] >= 0) kept[r] |= (rank++) << 1;
+    }
+    if (t == 0) ws.nkept[c] = nkt;
+}
+
+// R: one chunk.  Tile offsets (exclusive scan of the tile totals, in blocks of kIT tiles;
+// kept in LDS too for up to kToffLds tiles), then resolve_runs.
+constexpr int kToffLds = 1024;
+__global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int64_t C,
+                                                    IslWs ws) {
+    const int64_t c = blockIdx.x;
+    const int t = threadIdx.x, nl = blockDim.x;
+    const int64_t maxr = C / 2 + 1;
+    const uint32_t* pk = packed + c * (C / 16);
+    __shared__ Cnt5 s5[2][16];
+    __shared__ uint32_t sm[16];
+    __shared__ int32_t sk[16];
+    __shared__ Cnt5 s_to[kToffLds];
+    const bool in_lds = ws.ntile <= kToffLds;
+    Cnt5 carry{0, 0, 0, 0, 0};
+    for (int64_t b = 0, it = 0; b < ws.ntile; b += nl, ++it) {
+        const int64_t i = b + t;
+        const Cnt5 v = i < ws.ntile ? ws.ttot[c * ws.ntile + i] : Cnt5{0, 0, 0, 0, 0};
+        Cnt5 tot;
+        const Cnt5 e = wg_scan5(v, s5[it & 1], tot);   // double-buffered: one barrier per block
+        if (i < ws.ntile) {
+            const Cnt5 o = cadd(e, carry);
+            ws.toff[c * ws.ntile + i] = o;
+            if (in_lds) s_to[i] = o;
+        }
+        carry = cadd(carry, tot);
+    }
+    if (!in_lds) __threadfence();   // read back past L1 below
+    __syncthreads();
+    // closed runs only: an island still open at the chunk end is dropped (:269-339)
+    const int64_t nr = carry.cl;
+    if (t == 0) ws.ncloses[c] = (int32_t)nr;
+    int32_t* kept = ws.kept + c * maxr;
+    if (in_lds)
+        resolve_runs<false>(pk, ws, s_to, c, nr, kept, sm, sk);
+    else
+        resolve_runs<true>(pk, ws, ws.toff + c * ws.ntile, c, nr, kept, sm, sk);
+}
+
+__global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, int64_t C,
+                                               int64_t first_chunk, IslWs ws, cpg_island* out,
+                                               int64_t cap, int64_t* count,
                                                const int64_t* base_in) {
     const int64_t c = blockIdx.x;
     // the chunk's first record: kept islands of all earlier chunks (fixed-order sum)
@@ -388,12 +508,9 @@ __global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, const uin
     // *count receives the running total
     const int64_t base = sb[0] + (base_in ? *base_in : 0);
     if (c == (int64_t)gridDim.x - 1 && threadIdx.x == 0) *count = base + ws.nkept[c];
-    const int64_t nw = C / 32, maxr = C / 2 + 1;
+    const int64_t maxr = C / 2 + 1;
     const uint32_t* pk = packed + c * (C / 16);
-    const uint32_t* sg = sign + c * nw;
     const int64_t nr = ws.ncloses[c];
-    const uint32_t* st = ws.starts + c * maxr;
-    const uint32_t* cl = ws.closes + c * maxr;
     const int32_t* kept = ws.kept + c * maxr;
     const int64_t gchunk = first_chunk + c;
     const uint32_t cbase = (uint32_t)gchunk * (uint32_t)C;   // chunk*0x100000, Java int
@@ -402,7 +519,7 @@ __global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, const uin
         if (k < 0) continue;
         const int64_t dst = base + (k >> 1);
         if (dst >= cap) continue;
-        const RunStat rs = run_stat(pk, sg, ws, c, nw, st[r], cl[r]);
+        const RunStat rs = run_stat<false>(pk, ws, ws.toff + c * ws.ntile, c, r);
         const Rec o = filter(rs, (uint32_t)(k & 1));
         cpg_island isl;
         isl.beg1 = (int32_t)((uint32_t)rs.beg + cbase + 1u);          // :287
@@ -430,16 +547,12 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
     if (nchunks == 0)
         return base_in ? hipMemcpyAsync(count, base_in, sizeof(int64_t), hipMemcpyDeviceToDevice, s)
                        : hipMemsetAsync(count, 0, sizeof(int64_t), s);
-    const int ntiles = (int)((chunk_len / 32 + kTileW - 1) / kTileW);
-    Cnt5* tiles = static_cast<Cnt5*>(ws.tiles);
-    hipLaunchKernelGGL(k_isl_a1, dim3((unsigned)(nchunks * ntiles)), dim3(kAT), 0, s, packed,
-                       sign, chunk_len, ntiles, tiles);
-    hipLaunchKernelGGL(k_isl_a3, dim3((unsigned)(nchunks * ntiles)), dim3(kAT), 0, s, packed,
-                       sign, chunk_len, ntiles, tiles, ws);
-    hipLaunchKernelGGL(k_isl_b, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
+    hipLaunchKernelGGL(k_isl_tile, dim3((unsigned)(nchunks * ws.ntile)), dim3(kTT), 0, s, packed,
+                       sign, chunk_len, ws);
+    hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed,
                        chunk_len, ws);
-    hipLaunchKernelGGL(k_isl_d, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, sign,
-                       chunk_len, first_chunk, ws, out, cap, count, base_in);
+    hipLaunchKernelGGL(k_isl_d, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, chunk_len,
+                       first_chunk, ws, out, cap, count, base_in);
     return hipGetLastError();
 }
 

@@ -278,9 +278,46 @@ def test_islands_random_states_vs_oracle(gpu_ctx, torch_dev):
         assert np.array_equal(got, exp)
 
 
-def _rand_states(rng):
+@pytest.mark.parametrize("C", [1 << 17, 1 << 20])
+def test_islands_multi_tile_vs_oracle(gpu_ctx, torch_dev, C):
+    """Chunks of several 131,072-position tiles with runs across tile borders: 2^17 has
+    ~4k runs per chunk (several per lane, register-cached), 2^20 ~35k (re-read path)."""
+    from cpgisland_amd import device as D
+    rng = np.random.default_rng(C)
+    nch = 3
+    states = np.resize(_rand_states(rng, nch * C), nch * C)
+    obs = (states % 4).astype(np.uint8)
+    sg = (states < 4).astype(np.uint8)
+    dp, ds = _dev_genome(pr.pack(obs), pr.pack_bits(sg), torch_dev)
+    out, cnt = D.islands(gpu_ctx, dp, ds, nch * C, C, cap=1 << 16)
+    got = D.islands_to_numpy(out, cnt)
+    exp = np.concatenate([co.islands(states[c * C:(c + 1) * C], c) for c in range(nch)])
+    assert len(exp) > 1000
+    assert np.array_equal(got, exp)
+
+
+def test_islands_huge_chunk_vs_oracle(gpu_ctx, torch_dev):
+    """One chunk of 1,025 tiles: the tile offsets live in global memory, not LDS."""
+    from cpgisland_amd import device as D
+    C = (1 << 27) + (1 << 17)
+    st = np.full(C, 6, np.int32)
+    rng = np.random.default_rng(5)
+    for b in np.sort(rng.choice(C - 4000, 300, replace=False)):
+        L = int(rng.integers(2, 3000))
+        st[b:b + L] = np.resize(np.array([1, 2, 1, 2, 0, 3], np.int32), L)
+    st[(1 << 27) - 50:(1 << 27) + 50] = np.resize(np.array([1, 2], np.int32), 100)   # across
+    st[C - 200:C - 100] = 1                          # the last tile border; no G: dropped
+    dp, ds = _dev_genome(pr.pack((st % 4).astype(np.uint8)),
+                         pr.pack_bits((st < 4).astype(np.uint8)), torch_dev)
+    out, cnt = D.islands(gpu_ctx, dp, ds, C, C)
+    exp = co.islands(st, 0)
+    assert len(exp) > 100
+    assert np.array_equal(D.islands_to_numpy(out, cnt), exp)
+
+
+def _rand_states(rng, n=4096):
     out = []
-    while len(out) < 4096:
+    while len(out) < n:
         plus = rng.random() < 0.4
         L = int(rng.integers(1, 60))
         b = rng.choice(4, L, p=[0.15, 0.35, 0.35, 0.15] if plus else [0.3, 0.2, 0.2, 0.3])
