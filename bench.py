@@ -133,6 +133,10 @@ def main():
                     help="join both streams after every step (by default step k+1's training "
                          "pass may start while step k's decode still runs: the steps are "
                          "independent batches, pipelined for throughput)")
+    ap.add_argument("--lanes", type=int, default=1,
+                    help="pipeline lanes: step k runs on lane k %% lanes, each lane with its own "
+                         "context (workspace), stream pair and outputs, so consecutive steps' "
+                         "kernels of the same kind may run concurrently")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="write this many MiB of scratch between steps (cold Infinity Cache)")
     args = ap.parse_args()
@@ -165,16 +169,26 @@ def main():
     model0 = HmmModel.initial()
     ndec = N // DECODE
     first_chunk = start // DECODE
-    so = torch.empty(D.words32(N) + 4, dtype=torch.int32, device=dev)
-    score = torch.empty(max(ndec, 1), dtype=torch.float64, device=dev)
-    ecnt = torch.empty(105, dtype=torch.float64, device=dev)
-    lcnt = torch.empty(124, dtype=torch.int64, device=dev)
-    icap = 1 << 20
-    iout = torch.empty((icap, 32), dtype=torch.uint8, device=dev)
-    icnt = torch.zeros(1, dtype=torch.int64, device=dev)
     flush = torch.empty(args.flush_mb << 18, dtype=torch.float32, device=dev) if args.flush_mb else None
+    nlanes = 1 if (args.serial or args.no_overlap) else max(1, args.lanes)
+    icap = 1 << 20
+
+    def make_lane(cx):
+        return {"ctx": cx,
+                "so": torch.empty(D.words32(N) + 4, dtype=torch.int32, device=dev),
+                "score": torch.empty(max(ndec, 1), dtype=torch.float64, device=dev),
+                "ecnt": torch.empty(105, dtype=torch.float64, device=dev),
+                "lcnt": torch.empty(124, dtype=torch.int64, device=dev),
+                "iout": torch.empty((icap, 32), dtype=torch.uint8, device=dev),
+                "icnt": torch.zeros(1, dtype=torch.int64, device=dev)}
+    lanes = [make_lane(ctx)]
+    for _ in range(1, nlanes):
+        cx = Context(local)
+        cx.reserve(N)
+        lanes.append(make_lane(cx))
 
     # trained model for the decode: one Baum-Welch iteration from the reference's model
+    ecnt = lanes[0]["ecnt"]
     D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
     if dist:
         cdist.merge_counts_f64(ecnt)
@@ -194,48 +208,53 @@ def main():
     # join between steps (--no-overlap adds one).  --serial runs everything on one stream
     # (isolated phase times).
     main_s = torch.cuda.current_stream()
-    s_tr = main_s if args.serial else torch.cuda.Stream()
-    # the decode stream at high priority: its latency-bound kernels get CUs first as the
-    # E-step's workgroups retire, the E-step fills the rest
-    s_dec = main_s if args.serial else torch.cuda.Stream(priority=-1 if args.prio else 0)
+    for ln in lanes:
+        ln["s_tr"] = main_s if args.serial else torch.cuda.Stream()
+        # the decode stream at high priority: its latency-bound kernels get CUs first as the
+        # E-step's workgroups retire, the E-step fills the rest
+        ln["s_dec"] = main_s if args.serial else torch.cuda.Stream(priority=-1 if args.prio else 0)
 
-    def step(it):
-        def mark(k, i):
+    def step(it, k):
+        ln = lanes[k % nlanes]
+        cx, s_tr, s_dec = ln["ctx"], ln["s_tr"], ln["s_dec"]
+
+        def mark(name, i):
             if it is not None:
-                evs[it][k][i].record()
+                evs[it][name][i].record()
         if args.no_overlap or args.serial:
             s_tr.wait_stream(main_s)
             s_dec.wait_stream(main_s)
         with torch.cuda.stream(s_dec):
             mark("viterbi", 0)
-            D.viterbi(ctx, model1, dp, N, DECODE, sign_out=so, score=score)
+            D.viterbi(cx, model1, dp, N, DECODE, sign_out=ln["so"], score=ln["score"])
             mark("viterbi", 1)
             mark("islands", 0)
-            D.islands(ctx, dp, so, N, DECODE, cap=icap, first_chunk=first_chunk, out=iout,
-                      count=icnt)
+            D.islands(cx, dp, ln["so"], N, DECODE, cap=icap, first_chunk=first_chunk,
+                      out=ln["iout"], count=ln["icnt"])
             mark("islands", 1)
         with torch.cuda.stream(s_tr):
             mark("estep", 0)
-            D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
+            D.bw_estep(cx, model0, dp, N, TRAIN, out=ln["ecnt"])
             mark("estep", 1)
             mark("counts", 0)
-            D.count_labelled(ctx, dp, ds, N, TRAIN, out=lcnt)
+            D.count_labelled(cx, dp, ds, N, TRAIN, out=ln["lcnt"])
             mark("counts", 1)
             mark("reduce", 0)
             if dist:   # the reducer: int64 sums are exact in any order; fp64 in rank order
-                cdist.merge_counts_i64(lcnt)
-                cdist.merge_counts_f64(ecnt)
+                cdist.merge_counts_i64(ln["lcnt"])
+                cdist.merge_counts_f64(ln["ecnt"])
             mark("reduce", 1)
         if args.no_overlap or args.serial:
             main_s.wait_stream(s_tr)
             main_s.wait_stream(s_dec)
 
-    for _ in range(args.warmup):
-        step(None)
+    for w in range(args.warmup):
+        step(None, w)
         if flush is not None:
             flush.fill_(1.0)
     torch.cuda.synchronize()
-    ctx.sync(None)
+    for ln in lanes:
+        ln["ctx"].sync(None)
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -243,10 +262,11 @@ def main():
     for it in range(args.steps):
         if flush is not None:
             flush.fill_(1.0)
-        step(it)
+        step(it, it)
     issue = time.perf_counter() - t0   # host time to enqueue every step (launch-bound check)
-    main_s.wait_stream(s_tr)
-    main_s.wait_stream(s_dec)
+    for ln in lanes:
+        main_s.wait_stream(ln["s_tr"])
+        main_s.wait_stream(ln["s_dec"])
     torch.cuda.synchronize()
     for ev in evs:
         for k, (a, b) in ev.items():
@@ -255,7 +275,8 @@ def main():
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
-    ctx.sync(None)     # raises if any kernel self-check (exactness) failed
+    for ln in lanes:
+        ln["ctx"].sync(None)     # raises if any kernel self-check (exactness) failed
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -301,9 +322,10 @@ def main():
                           "streams": 1 if args.serial else 2,
                           "decode_priority": "high" if (args.prio and not args.serial) else "normal",
                           "step_overlap": not (args.no_overlap or args.serial),
+                          "pipeline_lanes": nlanes,
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
-                          "islands_found": int(icnt.item())},
+                          "islands_found": int(lanes[0]["icnt"].item())},
                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
                "host_issue_ms_per_step": round(issue * 1e3 / steps, 4),
                "roofline": roof, "roofline_decode": roof_decode}
@@ -313,7 +335,8 @@ def main():
         else:
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
-    ctx.close()
+    for ln in lanes:
+        ln["ctx"].close()
     if dist:
         torch.distributed.destroy_process_group()
 

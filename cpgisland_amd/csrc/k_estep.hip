@@ -27,6 +27,16 @@
 
 #include "cpg_internal.h"
 
+// The E-step is a tolerance-bound fp64 computation (unlike the bit-exact Viterbi): products
+// and sums may be contracted to FMAs here (the fixed-point conversion of a posterior becomes
+// one fma(x, rz, 1.5*2^52): a single rounding onto the integer grid).
+#ifndef EST_CONTRACT
+#define EST_CONTRACT 1
+#endif
+#if EST_CONTRACT
+#pragma clang fp contract(fast)
+#endif
+
 namespace cpg {
 namespace {
 
@@ -64,13 +74,18 @@ struct Mat {
     int e;               // value = 2^e * matrix
 };
 
+// floor(log2 mx) for finite mx > 0 (denormals included: v_frexp_exp), 0 for mx == 0 — a
+// select, not a branch, so independent normalisations (prefix / suffix scans, forward /
+// backward chains) interleave
+__device__ __forceinline__ int exp2_floor(double mx) {
+    const int k = __builtin_amdgcn_frexp_exp(mx) - 1;
+    return mx > 0.0 ? k : 0;
+}
 __device__ __forceinline__ void mnorm(Mat& m) {
     const double mx = fmax(fmax(m.a, m.b), fmax(m.c, m.d));
-    if (mx > 0.0) {
-        const int k = ilogb(mx);
-        m.a = ldexp(m.a, -k); m.b = ldexp(m.b, -k); m.c = ldexp(m.c, -k); m.d = ldexp(m.d, -k);
-        m.e += k;
-    }
+    const int k = exp2_floor(mx);
+    m.a = ldexp(m.a, -k); m.b = ldexp(m.b, -k); m.c = ldexp(m.c, -k); m.d = ldexp(m.d, -k);
+    m.e += k;
 }
 __device__ __forceinline__ Mat mmul(const Mat& x, const Mat& y) {
     Mat r{x.a * y.a + x.b * y.c, x.a * y.b + x.b * y.d, x.c * y.a + x.d * y.c,
@@ -79,6 +94,9 @@ __device__ __forceinline__ Mat mmul(const Mat& x, const Mat& y) {
     return r;
 }
 __device__ __forceinline__ Mat mid() { return {1.0, 0.0, 0.0, 1.0, 0}; }
+__device__ __forceinline__ Mat msel(bool c, const Mat& x, const Mat& y) {   // field selects
+    return {c ? x.a : y.a, c ? x.b : y.b, c ? x.c : y.c, c ? x.d : y.d, c ? x.e : y.e};
+}
 // product of two 2x2 matrices given as rows (x = row 0, y = row 1), not normalised
 __device__ __forceinline__ Mat mmul_raw(double2 xa, double2 xb, double2 ya, double2 yb) {
     return {xa.x * ya.x + xa.y * yb.x, xa.x * ya.y + xa.y * yb.y, xb.x * ya.x + xb.y * yb.x,
@@ -94,13 +112,9 @@ __device__ __forceinline__ Mat shfl_down_mat(const Mat& x, int d) {
 }
 
 __device__ __forceinline__ int vnorm(double& x, double& y) {   // returns the shift applied
-    const double mx = fmax(x, y);
-    int k = 0;
-    if (mx > 0.0) {
-        k = ilogb(mx);
-        x = ldexp(x, -k);
-        y = ldexp(y, -k);
-    }
+    const int k = exp2_floor(fmax(x, y));
+    x = ldexp(x, -k);
+    y = ldexp(y, -k);
     return k;
 }
 
@@ -284,8 +298,9 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const Mat yp = shfl_up_mat(xp, off), ys = shfl_down_mat(xs, off);
-        if (lane >= off) xp = mmul(yp, xp);
-        if (lane + off < 64) xs = mmul(xs, ys);
+        const Mat np = mmul(yp, xp), ns = mmul(xs, ys);
+        xp = msel(lane >= off, np, xp);
+        xs = msel(lane + off < 64, ns, xs);
     }
     const Mat up1 = shfl_up_mat(xp, 1), dn1 = shfl_down_mat(xs, 1);
     __syncthreads();   // every lane is past its 4-step table reads: the union is free
@@ -301,8 +316,9 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {
             const Mat yp = shfl_up_mat(wp, off), ys = shfl_down_mat(ws, off);
-            if (t >= off) wp = mmul(yp, wp);
-            if (t + off < 16) ws = mmul(ws, ys);
+            const Mat np = mmul(yp, wp), ns = mmul(ws, ys);
+            wp = msel(t >= off, np, wp);
+            ws = msel(t + off < 16, ns, ws);
         }
         const Mat ep = shfl_up_mat(wp, 1), es = shfl_down_mat(ws, 1);
         if (t < nw) {
@@ -417,16 +433,23 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
         // table rows of the next (lower) position are read one position ahead, before this
         // position's LDS atomics: LDS operations retire in order, so a read issued after the
         // atomics would make every position wait for the previous position's atomics
-#if EST_PF
+#if EST_PF == 1
         double2 pma = TA[code_at(cm, kMB - 1)], pmb = TB[code_at(cm, kMB - 1)];
+#elif EST_PF == 2
+        double2 pma = gtab[code_at(cm, kMB - 1)], pmb = gtab[16 + code_at(cm, kMB - 1)];
 #endif
 #pragma unroll
         for (int i = kMB - 1; i >= 0; --i) {
 #if EST_PF
             const double2 cma = pma, cmb = pmb;
             if (i > 0) {
+#if EST_PF == 2
+                pma = gtab[code_at(cm, i - 1)];
+                pmb = gtab[16 + code_at(cm, i - 1)];
+#else
                 pma = TA[code_at(cm, i - 1)];
                 pmb = TB[code_at(cm, i - 1)];
+#endif
             }
 #else
 #if EST_GTAB   // the same rows from a global copy: waited on with vmcnt, not behind the atomics
@@ -473,6 +496,7 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
                 atomicAdd(pb + 3, to_fixed_scaled(x11 * rz) + d);
             }
 #else
+            // to_fixed_scaled(x * rz) contracts to one fma(x, rz, 1.5*2^52)
             atomicAdd(wb + bin_of(d, 0), to_fixed_scaled(x00 * rz));
             atomicAdd(wb + bin_of(d, 1), to_fixed_scaled(x01 * rz));
             atomicAdd(wb + bin_of(d, 2), to_fixed_scaled(x10 * rz));
