@@ -159,13 +159,24 @@ struct Codes {
         return s == 0 ? (__builtin_amdgcn_alignbit(raw[r], lo, 30) & 0x3FFu)
                       : ((raw[r] >> (8 * s - 2)) & 0x3FFu);
     }
-    // the 16 codes of mini-block m (runtime m: a select chain, no register indexing)
+    // the 16 codes of mini-block m (m compile-time)
     __device__ __forceinline__ uint64_t mb(int m) const {
-        const uint32_t lo = m == 0 ? w[0] : m == 1 ? w[2] : m == 2 ? w[4] : w[6];
-        const uint32_t hi = m == 0 ? w[1] : m == 1 ? w[3] : m == 2 ? w[5] : w[7];
-        return ((uint64_t)hi << 32) | lo;
+        return ((uint64_t)w[2 * m + 1] << 32) | w[2 * m];
     }
 };
+// 16 2-bit fields -> 16 4-bit fields (in their low 2 bits)
+__device__ __forceinline__ uint64_t spread2(uint32_t v) {
+    uint64_t x = v;
+    x = (x | (x << 16)) & 0x0000FFFF0000FFFFull;
+    x = (x | (x << 8)) & 0x00FF00FF00FF00FFull;
+    x = (x | (x << 4)) & 0x0F0F0F0F0F0F0F0Full;
+    x = (x | (x << 2)) & 0x3333333333333333ull;
+    return x;
+}
+// the 16 dinucleotide codes (prev | cur << 2) of the packed word x; pb = the base before it
+__device__ __forceinline__ uint64_t codes16(uint32_t x, uint32_t pb) {
+    return spread2((x << 2) | pb) | (spread2(x) << 2);
+}
 __device__ __forceinline__ uint32_t code_at(uint64_t mb, int i) {   // i compile-time
     return (uint32_t)(mb >> (4 * i)) & 15u;
 }
@@ -368,7 +379,6 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     for (int i = t; i < nw * kNRep * kRep; i += nl) bins[i] = 0ull;
     __syncthreads();
     CPG_EST_MARK(T5)
-    const Codes cd = lane_codes(pk, t);   // 20 B from L2 again rather than 13 live VGPRs
     // 3b. mini-blocks, last to first: forward alphas in registers from the checkpoint, then
     //     backward with xi accumulation; beta flows on from one mini-block to the previous
     unsigned long long* wb = bins + ((t >> 6) * kNRep + lane / (64 / kNRep)) * kRep;
@@ -393,7 +403,11 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
 #endif
 #pragma unroll EST_MB_UNROLL
     for (int m = NMB - 1; m >= 0; --m) {
-        const uint64_t cm = cd.mb(m);   // (codes re-derived after the scans: see 3a)
+        // the mini-block's codes from its packed word (L1/L2, two dwords): neither 8 live
+        // VGPRs of codes nor a scratch copy of them
+        const uint32_t xw = pk[4 * t + m];
+        const uint32_t pw = (t > 0 || m > 0) ? pk[4 * t + m - 1] : 0u;
+        const uint64_t cm = codes16(xw, pw >> 30);
         // alpha at the position before the mini-block (select chain: no register indexing)
         double bfP = aP, bfM = aM;
         if (m > 0) {
