@@ -80,6 +80,36 @@ int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitT
     return CPG_OK;
 }
 
+// the E-step's one-step tables, cached per model like the Viterbi tables: rows
+// TA[d] = (a[p][b], a[p][b+4]), TB[d] = (a[p+4][b], a[p+4][b+4]) for d = p | b << 2 (p the
+// previous base, b the current one) — written once per model instead of a kernel per call
+int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out) {
+    for (int i = 0; i < ctx->etn; ++i)
+        if (std::memcmp(&ctx->etc_[i].model, m, sizeof *m) == 0) {
+            *out = ctx->etc_[i].d;
+            return CPG_OK;
+        }
+    cpg_ctx::EtSlot* sl;
+    if (ctx->etn < cpg_ctx::kVtSlots) {
+        sl = &ctx->etc_[ctx->etn++];
+        CPG_HIP(hipMalloc(&sl->d, 32 * sizeof(double2)));
+    } else {
+        sl = &ctx->etc_[ctx->etnext];
+        ctx->etnext = (ctx->etnext + 1) % cpg_ctx::kVtSlots;
+        CPG_HIP(hipDeviceSynchronize());   // the evicted slot may still be read
+    }
+    double2 h[32];
+    for (int d = 0; d < 16; ++d) {
+        const int p = d & 3, b = d >> 2;
+        h[d] = make_double2(m->a[p][b], m->a[p][b + 4]);
+        h[16 + d] = make_double2(m->a[p + 4][b], m->a[p + 4][b + 4]);
+    }
+    sl->model = *m;
+    CPG_HIP(hipMemcpy(sl->d, h, sizeof h, hipMemcpyHostToDevice));
+    *out = sl->d;
+    return CPG_OK;
+}
+
 namespace {
 
 int check_layout(const void* packed, int64_t nbases, int64_t chunk_len) {
@@ -131,6 +161,7 @@ void cpg_close(cpg_ctx* ctx) {
         if (b.p) (void)hipHostFree(b.p);
     if (ctx->d_status) (void)hipFree(ctx->d_status);
     for (int i = 0; i < ctx->vtn; ++i) (void)hipFree(ctx->vtc[i].d);
+    for (int i = 0; i < ctx->etn; ++i) (void)hipFree(ctx->etc_[i].d);
     for (auto& ps : ctx->ps)
         if (ps) (void)hipStreamDestroy(ps);
     for (auto& ev : ctx->pev)
@@ -208,11 +239,14 @@ int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed
     std::lock_guard<std::mutex> lk(ctx->mu);
     CPG_HIP(hipSetDevice(ctx->device));
     hipStream_t s = pick(ctx, stream);
-    // undecoded tail -> '-' bits (whole words past the last chunk)
+    // undecoded tail -> '-' bits (whole words past the last chunk): zeroed by the traceback
+    // launch, or here when there is no chunk to decode
     const int64_t w_done = (nch * chunk_len + 31) / 32, w_all = (nbases + 31) / 32;
-    if (w_all > w_done)
-        CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)(w_all - w_done) * 4, s));
-    if (nch == 0) return CPG_OK;
+    const int64_t ntail = w_all > w_done ? w_all - w_done : 0;
+    if (nch == 0) {
+        if (ntail) CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)ntail * 4, s));
+        return CPG_OK;
+    }
     VitConsts vc;
     static thread_local VitTables vt;
     if ((rc = vit_prepare(model, chunk_len, &vc, &vt))) return rc;
@@ -222,7 +256,8 @@ int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed
     const size_t need = viterbi_ws_bytes(nch, chunk_len);
     if ((rc = ws_get(ctx, WS_VIT, need, &ws))) return rc;
     CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
-                           d_sign_out, d_score, nullptr, ctx->d_status, s));
+                           d_sign_out, d_score, nullptr, ctx->d_status, s, d_sign_out + w_done,
+                           ntail));
     return CPG_OK;
 }
 
@@ -274,8 +309,10 @@ int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packe
     const int64_t nch = nbases / chunk_len;
     void* ws;
     if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nch, chunk_len), &ws))) return rc;
+    const double2* gtab = nullptr;
+    if (nch > 0 && (rc = est_tables(ctx, model, &gtab))) return rc;
     CPG_HIP(launch_estep(*model, d_packed, nch, chunk_len, (unsigned long long*)ws, d_counts,
-                         pick(ctx, stream)));
+                         pick(ctx, stream), PART_ALL, gtab));
     return CPG_OK;
 }
 

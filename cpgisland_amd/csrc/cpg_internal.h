@@ -85,6 +85,12 @@ struct cpg_ctx {
         cpg::VitTables* d;
     } vtc[kVtSlots];
     int vtn = 0, vtnext = 0;
+    // device copies of per-model E-step one-step tables (rows TA | TB, 32 x double2)
+    struct EtSlot {
+        cpg_model model;
+        double2* d;
+    } etc_[kVtSlots];
+    int etn = 0, etnext = 0;
     // streamed-genome pipeline (cpg_genome_run): copy-in, train, decode, copy-out streams
     // and per-buffer events, created on first use
     hipStream_t ps[4] = {};
@@ -98,6 +104,7 @@ int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out);
 int model_check_deterministic(const cpg_model* m);
 bool aligned16(const void* p);
 int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitTables** out);
+int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out);
 enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
        WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9, WS_GEN = 10, WS_GISL = 11, WS_CSORT = 12,
        WS_CBP = 13, WS_CISL = 14, WS_CCK = 15 };
@@ -115,7 +122,8 @@ size_t count_ws_bytes(int64_t nchunks);
 hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint32_t* packed,
                           int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
                           uint32_t* sign_out, double* score, uint8_t* degen,
-                          uint32_t* status, hipStream_t s);
+                          uint32_t* status, hipStream_t s, uint32_t* zero_at = nullptr,
+                          int64_t zero_n = 0);
 size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len);
 int64_t vit_nsb(int64_t chunk_len);
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
@@ -123,9 +131,10 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
                           cpg_island* out, int64_t cap, int64_t* count, hipStream_t s,
                           const int64_t* base_in = nullptr);
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
+// gtab: the model's one-step tables in device memory (est_tables); needed with PART_ACC
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t chunk_len, unsigned long long* acc, double* out,
-                        hipStream_t s, int parts = PART_ALL);
+                        hipStream_t s, int parts = PART_ALL, const double2* gtab = nullptr);
 size_t estep_ws_bytes(int64_t nchunks, int64_t chunk_len);
 
 // ragged contig batches (k_contigs.hip)

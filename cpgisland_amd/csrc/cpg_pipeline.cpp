@@ -118,6 +118,8 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
     const int64_t wdec = W / D, wtr = W / T;
     if (counts_out && (rc = ws_get(ctx, WS_COUNT, count_ws_bytes(wtr), &ws_cnt))) return rc;
     if (estep_out && (rc = ws_get(ctx, WS_EST, estep_ws_bytes(wtr, T), &ws_est))) return rc;
+    const double2* est_gtab = nullptr;
+    if (estep_out && (rc = est_tables(ctx, train_model, &est_gtab))) return rc;
     if (decode && (rc = ws_get(ctx, WS_VIT, viterbi_ws_bytes(wdec, D), &ws_vit))) return rc;
     if (decode && (rc = ws_get(ctx, WS_ISL, islands_ws_bytes(wdec, D), &ws_isl))) return rc;
     // window buffers + results, one allocation
@@ -173,7 +175,7 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
         if (estep_out && ntr > 0)
             CPG_HIP(launch_estep(*train_model, buf_packed(b), ntr, T,
                                  static_cast<unsigned long long*>(ws_est), nullptr, str,
-                                 PART_ACC));
+                                 PART_ACC, est_gtab));
         if (counts_out && ntr > 0)
             CPG_HIP(launch_count(buf_packed(b), buf_sign(b), ntr, T, static_cast<uint64_t*>(ws_cnt),
                                  nullptr, str, PART_ACC));

@@ -558,15 +558,6 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
 #endif
 }
 
-// the 1-step tables of the model in global memory (rows TA | TB), for EST_GTAB
-__global__ void k_estep_tabs(const cpg_model model, double2* __restrict__ gtab) {
-    const int t = threadIdx.x;
-    if (t < 16) {
-        const int p = t & 3, b = t >> 2;
-        gtab[t] = make_double2(model.a[p][b], model.a[p][b + 4]);
-        gtab[16 + t] = make_double2(model.a[p + 4][b], model.a[p + 4][b + 4]);
-    }
-}
 
 __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 
@@ -627,7 +618,7 @@ size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t C, unsigned long long* acc, double* out, hipStream_t s,
-                        int parts) {
+                        int parts, const double2* gtab) {
     if (C % 4096 || C > (int64_t)kET * kLanePos) return hipErrorInvalidValue;
     if (nchunks == 0 && parts == PART_ALL)
         return hipMemsetAsync(out, 0, 105 * sizeof(double), s);
@@ -636,10 +627,9 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
         const size_t uni = kUnionBytes;   // sized for 16 waves; fewer lanes use a prefix
         const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long) +
                            (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
-        double2* gtab = reinterpret_cast<double2*>(acc + 2 * kSlab * kAccRep);
-        if (EST_GTAB) hipLaunchKernelGGL(k_estep_tabs, dim3(1), dim3(64), 0, s, model, gtab);
+        if (!gtab) return hipErrorInvalidValue;   // est_tables
         hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
-                           packed, C, acc, (const double2*)gtab);
+                           packed, C, acc, gtab);
     }
     if (parts & PART_FINAL)
         hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);

@@ -641,11 +641,16 @@ __device__ void vit_irregular(const VitConsts& vc, const uint32_t* packed, const
         if (split) {
             const int ia = max(0, min(nb - 1, e - vc.emin)) * 16;
             const int ib = max(0, min(nb - 1, e + 1 - vc.emin)) * 16;
+            // two walks, one per composite: a step choosing between `pre` and `post` at run
+            // time makes the compiler address them through memory (scratch)
             walk_piece(pk, k, gi, j0, jend, [&](uint32_t d, int j) {
                 if (j < t1) {
                     const double2 a = sA[ia + d], b = sB[ia + d];
                     c64_step(pre, a.x, a.y, b.x, b.y);
-                } else if (j >= t2) {
+                }
+            });
+            walk_piece(pk, k, gi, j0, jend, [&](uint32_t d, int j) {
+                if (j >= t2) {
                     const double2 a = sA[ib + d], b = sB[ib + d];
                     c64_step(post, a.x, a.y, b.x, b.y);
                 }
@@ -1105,8 +1110,11 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
 __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __restrict__ bp,
                                                         const uint8_t* __restrict__ endst,
                                                         uint32_t* __restrict__ sign_out,
-                                                        uint32_t* status) {
+                                                        uint32_t* status, uint32_t* zero_at,
+                                                        int64_t zero_n) {
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    // the undecoded tail's sign words ('-'), in this launch rather than a memset of its own
+    for (int64_t i = gid; i < zero_n; i += (int64_t)gridDim.x * kThreads) zero_at[i] = 0u;
     if (gid >= g.nchunks * g.nsb) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     uint32_t wP[8], wM[8];
@@ -1224,7 +1232,7 @@ size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len) {
 hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint32_t* packed,
                           int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
                           uint32_t* sign_out, double* score, uint8_t* degen_out,
-                          uint32_t* status, hipStream_t s) {
+                          uint32_t* status, hipStream_t s, uint32_t* zero_at, int64_t zero_n) {
     const int64_t nsb = vit_nsb(chunk_len);
     VitWs w = carve(ws, nchunks, nsb);
     if (w.bytes > ws_bytes) return hipErrorInvalidValue;
@@ -1249,7 +1257,7 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     hipLaunchKernelGGL(k_vit_tscan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, g, w.entry,
                        w.origin, w.endst, score);
     hipLaunchKernelGGL(k_vit_trace, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst, sign_out,
-                       status);
+                       status, zero_at, zero_n);
     if (degen_out) {
         hipError_t e = hipMemcpyAsync(degen_out, w.degen, nchunks, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;
