@@ -764,6 +764,8 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     const int cnt = (int)(b1 - b0);
     const bool pre = cnt > 0 && cnt <= kPre;   // cnt == 0: the generic loops do nothing
     // block b0 + i's plan and composites (i < cnt; callers unroll i)
+// (the post composite B is read for SPLIT blocks only: this one workgroup per chunk streams
+// its chunk's block records at one CU's share of the memory system)
 #define CPG_PREFETCH(P, A, B)                                  \
     VitPlan P[kPre];                                           \
     C64 A[kPre], B[kPre];                                      \
@@ -771,7 +773,10 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         const int64_t kk = b0 + (i < cnt ? i : 0);             \
         P[i] = pl[kk];                                         \
         A[i] = ld_c64(cp + 2 * kk);                            \
-        B[i] = ld_c64(cp + 2 * kk + 1);                        \
+    }                                                          \
+    _Pragma("unroll") for (int i = 0; i < kPre; ++i) {         \
+        const int64_t kk = b0 + (i < cnt ? i : 0);             \
+        B[i] = P[i].type == PLAN_SPLIT ? ld_c64(cp + 2 * kk + 1) : c64_id(); \
     }
     C64 run = c64_id(), lead = c64_id();
     bool hasb = false;
@@ -821,8 +826,10 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         if (lane >= d) x = seg_comb(y, x);
     }
     __shared__ Seg sWave[kChainT / 64];
+    CPG_CHAIN_MARK(T1a)
     if (lane == 63) sWave[wv] = x;
     __syncthreads();
+    CPG_CHAIN_MARK(T1b)
     Seg before{c64_id(), 0, 0};   // everything before this wave
     for (int w = 0; w < wv; ++w) before = seg_comb(before, sWave[w]);
     const Seg prev = seg_shfl_up(x, 1);   // inclusive value of the lane before
@@ -845,6 +852,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
             }
         }
     }
+    CPG_CHAIN_MARK(T1c)
     __syncthreads();
     CPG_CHAIN_MARK(T2)
     // phase 3: the serial chain over barriers.  The whole workgroup first stages every
@@ -953,9 +961,10 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     CPG_CHAIN_MARK(T5)
 #ifdef CPG_DEBUG_CHAIN
     if (t == 0 && (c == 0 || c == g.nchunks - 1))
-        printf("chain c%lld nbar %d: phase1 %llu scan %llu list+stage %llu serial %llu entries %llu"
-               " (wall-clock ticks)\n", (long long)c, nbar, T1 - T0, T2 - T1, T3 - T2, T4 - T3,
-               T5 - T4);
+        printf("chain c%lld nbar %d: phase1 %llu scan %llu (shfl %llu bar1 %llu combine+list %llu "
+               "bar2 %llu) list+stage %llu serial %llu entries %llu (wall-clock ticks)\n",
+               (long long)c, nbar, T1 - T0, T2 - T1, T1a - T1, T1b - T1a, T1c - T1b, T2 - T1c,
+               T3 - T2, T4 - T3, T5 - T4);
 #endif
 }
 
