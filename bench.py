@@ -137,6 +137,11 @@ def main():
                     help="pipeline lanes: step k runs on lane k %% lanes, each lane with its own "
                          "context (workspace), stream pair and outputs, so consecutive steps' "
                          "kernels of the same kind may run concurrently")
+    ap.add_argument("--train-cus", type=int, default=0,
+                    help="run the training pass on this many compute units only (a CU-masked "
+                         "stream), leaving the rest to the decode; 0 = all")
+    ap.add_argument("--train-cu-stride", type=int, default=0,
+                    help="with --train-cus: leave out every k-th CU instead of the last ones")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="write this many MiB of scratch between steps (cold Infinity Cache)")
     args = ap.parse_args()
@@ -208,8 +213,17 @@ def main():
     # join between steps (--no-overlap adds one).  --serial runs everything on one stream
     # (isolated phase times).
     main_s = torch.cuda.current_stream()
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    if args.train_cus and not args.serial:
+        if args.train_cu_stride:
+            tr_cus = [i for i in range(ncu) if i % args.train_cu_stride != 0][:args.train_cus]
+        else:
+            tr_cus = list(range(args.train_cus))
+    else:
+        tr_cus = None
     for ln in lanes:
-        ln["s_tr"] = main_s if args.serial else torch.cuda.Stream()
+        ln["s_tr"] = (main_s if args.serial else
+                      D.cu_stream(local, tr_cus) if tr_cus else torch.cuda.Stream())
         # the decode stream at high priority: its latency-bound kernels get CUs first as the
         # E-step's workgroups retire, the E-step fills the rest
         ln["s_dec"] = main_s if args.serial else torch.cuda.Stream(priority=-1 if args.prio else 0)
@@ -323,6 +337,7 @@ def main():
                           "decode_priority": "high" if (args.prio and not args.serial) else "normal",
                           "step_overlap": not (args.no_overlap or args.serial),
                           "pipeline_lanes": nlanes,
+                          "train_cus": len(tr_cus) if tr_cus else ncu,
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
                           "islands_found": int(lanes[0]["icnt"].item())},

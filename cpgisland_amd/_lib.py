@@ -59,6 +59,8 @@ SIGNATURES = {
     "cpg_abi_version": [],
     "cpg_reserve": [_P, _I64],
     "cpg_sync": [_P, _P],
+    "cpg_stream_create_cu": [_INT, _P, _INT, _P],
+    "cpg_stream_destroy": [_P],
     "cpg_initial_model": [_P],
     "cpg_ingest": [C.c_char_p, C.c_size_t, _INT, _INT, _P, _I64, _P],
     "cpg_synth": [C.c_uint64, _I64, _I64, _P, _P, _INT],

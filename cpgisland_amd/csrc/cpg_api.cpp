@@ -184,6 +184,22 @@ int cpg_reserve(cpg_ctx* ctx, int64_t nbases) {
     return CPG_OK;
 }
 
+int cpg_stream_create_cu(int device, const uint32_t* cu_mask, int mask_words, void** out) {
+    if (!out || !cu_mask || mask_words <= 0) return set_error(CPG_E_INVALID, "null argument");
+    *out = nullptr;
+    CPG_HIP(hipSetDevice(device));
+    hipStream_t s;
+    CPG_HIP(hipExtStreamCreateWithCUMask(&s, (uint32_t)mask_words, cu_mask));
+    *out = s;
+    return CPG_OK;
+}
+
+int cpg_stream_destroy(void* stream) {
+    if (!stream) return set_error(CPG_E_INVALID, "null stream");
+    CPG_HIP(hipStreamDestroy(static_cast<hipStream_t>(stream)));
+    return CPG_OK;
+}
+
 int cpg_sync(cpg_ctx* ctx, void* stream) {
     if (!ctx) return set_error(CPG_E_INVALID, "null ctx");
     CPG_HIP(hipSetDevice(ctx->device));

@@ -63,6 +63,14 @@ constexpr int kRep = EST_REP;
 #define EST_NREP 4
 #endif
 constexpr int kNRep = EST_NREP;   // bin replicas per wave (64 / kNRep lanes share one)
+// EST_BINS 1: one bin set of 64 rows (d, k) x 16 columns (u64), lane column = lane % 16.
+// An LDS 64-bit access serves 16 lanes per cycle with bank = (address / 4) mod 32: the 16
+// lanes of a pass always hit 16 different columns = 32 different banks, whatever their
+// classes — no bank conflicts and no same-address collisions inside a pass (the replicated
+// per-wave sets of EST_BINS 0 collide whenever two lanes of a pass share a class).
+#ifndef EST_BINS
+#define EST_BINS 1
+#endif
 // LDS: TA/TB (512 B) | union { 4-step tables, scan buffer, bins } | per-wave partials
 constexpr size_t kUnionOff = 32 * 16;
 constexpr size_t kUnionBytes =
@@ -376,12 +384,22 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     // 3a. bins (aliasing the scan buffer, read above) zeroed; alpha entering mini-block m
     //     = alpha entering the lane times phase 1's product of the first m mini-blocks
     //     (any per-position scale cancels in the normalised xi)
+#if EST_BINS
+    for (int i = t; i < 64 * 16; i += nl) bins[i] = 0ull;
+#else
     for (int i = t; i < nw * kNRep * kRep; i += nl) bins[i] = 0ull;
+#endif
     __syncthreads();
     CPG_EST_MARK(T5)
     // 3b. mini-blocks, last to first: forward alphas in registers from the checkpoint, then
     //     backward with xi accumulation; beta flows on from one mini-block to the previous
+#if EST_BINS
+    unsigned long long* wb = bins + (lane & 15);
+    constexpr int kBS = 16;   // row stride
+#else
     unsigned long long* wb = bins + ((t >> 6) * kNRep + lane / (64 / kNRep)) * kRep;
+    constexpr int kBS = 1;
+#endif
     double g0P = 0.0, g0M = 0.0;
     double yP = bP, yM = bM;   // beta at the last position of the mini-block
 #ifndef EST_ABL
@@ -511,10 +529,10 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
             }
 #else
             // to_fixed_scaled(x * rz) contracts to one fma(x, rz, 1.5*2^52)
-            atomicAdd(wb + bin_of(d, 0), to_fixed_scaled(x00 * rz));
-            atomicAdd(wb + bin_of(d, 1), to_fixed_scaled(x01 * rz));
-            atomicAdd(wb + bin_of(d, 2), to_fixed_scaled(x10 * rz));
-            atomicAdd(wb + bin_of(d, 3), to_fixed_scaled(x11 * rz));
+            atomicAdd(wb + bin_of(d, 0) * kBS, to_fixed_scaled(x00 * rz));
+            atomicAdd(wb + bin_of(d, 1) * kBS, to_fixed_scaled(x01 * rz));
+            atomicAdd(wb + bin_of(d, 2) * kBS, to_fixed_scaled(x10 * rz));
+            atomicAdd(wb + bin_of(d, 3) * kBS, to_fixed_scaled(x11 * rz));
 #endif
             yP = t00 + t01;
             yM = t10 + t11;
@@ -525,12 +543,22 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     CPG_EST_MARK(T6)
     // chunk totals of the nw * kNRep replicas: wave q sums replicas q, q + nw, ... of every
     // bin (integer sums: exact in any order), then 64 lanes add the nw partials
+#if EST_BINS
+    if (t < 64) {   // row t = d * 4 + k: the sum of its 16 columns
+        const unsigned long long* row = bins + bin_of(t >> 2, t & 3) * 16;
+        unsigned long long s = 0;
+#pragma unroll
+        for (int col = 0; col < 16; ++col) s += row[(col + t) & 15];   // rotated: no conflicts
+        part[t] = s;
+    }
+#else
     {
         const int q = t >> 6, b = bin_of(lane >> 2, lane & 3);   // lane = slab row d*4+k
         unsigned long long s = 0;
         for (int r = q; r < nw * kNRep; r += nw) s += bins[r * kRep + b];
         part[q * 64 + lane] = s;
     }
+#endif
     __syncthreads();
     CPG_EST_MARK(T7)
     unsigned long long* racc = acc + 2 * kSlab * (c % kAccRep);
@@ -538,7 +566,11 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     // 2^-47 units, the log-likelihood in signed 2^-24 units
     if (t < 64) {   // row t = d * 4 + k
         unsigned long long s = 0;
+#if EST_BINS
+        s = part[t];
+#else
         for (int q = 0; q < nw; ++q) s += part[q * 64 + t];
+#endif
         acc128_add(racc + 2 * t, s, false);
     }
     if (EST_ABL && sink == 0x123456789ull) acc[0] = sink;   // keep the ablated work live

@@ -25,6 +25,18 @@ def _stream():
     return C.c_void_p(torch.cuda.current_stream().cuda_stream)
 
 
+def cu_stream(device_index: int, cus) -> "torch.cuda.ExternalStream":
+    """A stream whose kernels run only on the compute units `cus` (cpg_stream_create_cu),
+    wrapped for torch (events, `torch.cuda.stream(...)`); lives until process exit."""
+    ncu = torch.cuda.get_device_properties(device_index).multi_processor_count
+    words = np.zeros((ncu + 31) // 32, np.uint32)
+    for cu in cus:
+        words[cu // 32] |= np.uint32(1 << (cu % 32))
+    h = C.c_void_p()
+    check(lib.cpg_stream_create_cu(device_index, ptr(words), len(words), C.byref(h)))
+    return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", device_index))
+
+
 def words16(nbases: int) -> int:
     return (nbases + 15) // 16
 

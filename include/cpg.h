@@ -111,6 +111,13 @@ int         cpg_reserve(cpg_ctx* ctx, int64_t nbases);
 /* Wait for `stream` and return the first kernel-reported status since the last
  * cpg_sync (CPG_OK or CPG_E_VERIFY / CPG_E_UNSUPPORTED). */
 int         cpg_sync(cpg_ctx* ctx, void* stream);
+/* A HIP stream whose kernels run only on the compute units set in cu_mask (mask_words
+ * 32-bit words, bit i = compute unit i in the runtime's order): partitions the GPU between
+ * concurrently running stages, e.g. the training pass and the latency-bound decode.
+ * Pass it as `stream` to the _d entry points; destroy with cpg_stream_destroy. */
+int         cpg_stream_create_cu(int device, const uint32_t* cu_mask, int mask_words,
+                                 void** out);
+int         cpg_stream_destroy(void* stream);
 
 /* ---- host utilities (no device) ---------------------------------------------- */
 /* The reference's initial model, CpGIslandFinder.java:155-173. */
