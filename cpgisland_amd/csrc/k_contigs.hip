@@ -261,7 +261,10 @@ __global__ __launch_bounds__(kCT) void k_ctg_viterbi(Ctg a, VitConsts vc,
 // ------------------------------------------------------------------ E-step
 constexpr double kFixC = 274877906944.0;            // 2^38 (contig bins; see header)
 constexpr double kMagic = 6755399441055744.0;       // 1.5 * 2^52
-constexpr int kNRep = 4, kRep = 80;                 // bin replicas per wave, padded stride
+// xi bins: 64 rows (k * 16 + d) x 16 lane columns (column = lane % 16): the 16 lanes of an
+// LDS 64-bit pass hit 16 columns = 32 distinct banks whatever their classes (no conflicts,
+// no same-address collisions); a column sums <= kCT / 16 lanes' contigs of <= 2^20 bases
+// in 2^-38 units: below 2^62 for kCT <= 256
 constexpr int kLogFix = 24;
 __device__ __forceinline__ unsigned long long to_fixed_scaled(double y) {
     return (unsigned long long)__double_as_longlong(y + kMagic) -
@@ -299,7 +302,8 @@ __global__ __launch_bounds__(kCT, CTG_EST_WAVES) void k_ctg_estep(Ctg a, cpg_mod
                                                    double2* __restrict__ ck,
                                                    unsigned long long* __restrict__ acc) {
     __shared__ double2 TA[16], TB[16];   // rows of M_d: (M(+,+), M(+,-)), (M(-,+), M(-,-))
-    __shared__ unsigned long long bins[kCT / 64 * kNRep * kRep];
+    __shared__ unsigned long long bins[64 * 16];
+    static_assert(kCT <= 256, "bin column capacity");
     __shared__ unsigned long long sinit[8];
     __shared__ long long sll;
     __shared__ double2 sent[3][kCT];     // alpha entering mini-blocks 1..3, per lane
@@ -310,10 +314,10 @@ __global__ __launch_bounds__(kCT, CTG_EST_WAVES) void k_ctg_estep(Ctg a, cpg_mod
         TB[t] = make_double2(model.a[p + 4][b], model.a[p + 4][b + 4]);
     }
     const uint4* pk4 = reinterpret_cast<const uint4*>(a.packed);
-    unsigned long long* wb = bins + ((t >> 6) * kNRep + lane / (64 / kNRep)) * kRep;
+    unsigned long long* wb = bins + (lane & 15);
     const int64_t stride = (int64_t)gridDim.x * kCT;
     for (int64_t g0 = (int64_t)blockIdx.x * kCT; g0 < a.n; g0 += stride) {
-        for (int i = t; i < kCT / 64 * kNRep * kRep; i += kCT) bins[i] = 0ull;
+        for (int i = t; i < 64 * 16; i += kCT) bins[i] = 0ull;
         if (t < 8) sinit[t] = 0ull;
         if (t == 0) sll = 0;
         __syncthreads();
@@ -443,10 +447,10 @@ __global__ __launch_bounds__(kCT, CTG_EST_WAVES) void k_ctg_estep(Ctg a, cpg_mod
                         const double x00 = uP * t00, x01 = uP * t01, x10 = uM * t10,
                                      x11 = uM * t11;
                         const double r = rcp_nr((x00 + x01) + (x10 + x11)) * kFixC;
-                        atomicAdd(wb + 0 * 16 + d, to_fixed_scaled(x00 * r));
-                        atomicAdd(wb + 1 * 16 + d, to_fixed_scaled(x01 * r));
-                        atomicAdd(wb + 2 * 16 + d, to_fixed_scaled(x10 * r));
-                        atomicAdd(wb + 3 * 16 + d, to_fixed_scaled(x11 * r));
+                        atomicAdd(wb + (0 * 16 + d) * 16, to_fixed_scaled(x00 * r));
+                        atomicAdd(wb + (1 * 16 + d) * 16, to_fixed_scaled(x01 * r));
+                        atomicAdd(wb + (2 * 16 + d) * 16, to_fixed_scaled(x10 * r));
+                        atomicAdd(wb + (3 * 16 + d) * 16, to_fixed_scaled(x11 * r));
                         yP = t00 + t01;
                         yM = t10 + t11;
                         if ((j & 3) == 0) vnorm(yP, yM);
@@ -458,7 +462,8 @@ __global__ __launch_bounds__(kCT, CTG_EST_WAVES) void k_ctg_estep(Ctg a, cpg_mod
         // flush: bins (2^-38) -> the 128-bit accumulators (2^-47): shift by 9
         if (t < 64) {   // t = k * 16 + d  ->  slab row d * 4 + k
             unsigned long long s = 0;
-            for (int r = 0; r < kCT / 64 * kNRep; ++r) s += bins[r * kRep + t];
+#pragma unroll
+            for (int col = 0; col < 16; ++col) s += bins[t * 16 + ((col + t) & 15)];
             if (s) acc128_add2(acc + 2 * ((t & 15) * 4 + (t >> 4)), s << 9, s >> 55);
         } else if (t < 72) {
             const unsigned long long s = sinit[t - 64];
