@@ -346,7 +346,7 @@ __device__ __forceinline__ bool binade_ok(const VitConsts& vc, int e) {
 }
 
 // K2 (one workgroup of 1024 lanes per chunk): scan of the K1 composites -> approximate
-// value entering every block (fixed point, int64; aent[nsb] = value after the last block),
+// value entering every block (fixed point, int64; stored for the irregular blocks),
 // then every block is classified from its entry/exit estimates: REGULAR (inside one
 // binade) or irregular (listed for K3b); block 0 is always sequential; DEGEN chunks (pi = 0
 // for both live states) skip everything.
@@ -422,14 +422,16 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
     if (t > 0) ci_apply(P, M, excl);
     for (int64_t k = b0; k < b1; ++k) {
         const longlong2 en = make_longlong2(P, M);
-        ae[k] = en;
         const int4 x = cc[k];
         ci_apply(P, M, CI{x.x, x.y, x.z, x.w});
         bool irregular;
         pl[k] = classify(vc, g, k, en, make_longlong2(P, M), irregular);
-        if (irregular) irrlist[c * g.nsb + atomicAdd(&sIrr, 1)] = (int32_t)k;
+        if (irregular) {   // only K3b reads the entry estimates (one workgroup writes a
+                           // chunk's records at one CU's share of the memory system)
+            ae[k] = en;
+            irrlist[c * g.nsb + atomicAdd(&sIrr, 1)] = (int32_t)k;
+        }
     }
-    if (b1 == g.nsb && b0 < b1) ae[g.nsb] = make_longlong2(P, M);
     __syncthreads();
     if (t == 0) irrcount[c] = sIrr;
 }
@@ -1097,17 +1099,21 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
     if (t == 0 && score) score[c] = s_end ? fin.x : fin.y;
     uint32_t F = 0x2u;
     for (int64_t k = b0; k < b1; ++k) F = map_compose(F, og[k]);
-    __shared__ uint32_t sF[kThreads];
-    sF[t] = F;
-    __syncthreads();
-    for (int off = 1; off < kThreads; off <<= 1) {
-        uint32_t x = sF[t];
-        if (t + off < kThreads) x = map_compose(x, sF[t + off]);
-        __syncthreads();
-        sF[t] = x;
-        __syncthreads();
+    // suffix composition over the lanes: wave shuffles (down), then the wave totals
+    const int lane = t & 63, wv = t >> 6;
+    uint32_t x = F;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_down(x, off);
+        if (lane + off < 64) x = map_compose(x, y);
     }
-    const uint32_t G = (t + 1 < kThreads) ? sF[t + 1] : 0x2u;
+    __shared__ uint32_t sW[kThreads / 64];
+    if (lane == 0) sW[wv] = x;
+    __syncthreads();
+    uint32_t after = 0x2u;   // composition of the waves after this one
+    for (int w = kThreads / 64 - 1; w > wv; --w) after = map_compose(sW[w], after);
+    const uint32_t dn = __shfl_down(x, 1);
+    const uint32_t G = lane < 63 ? map_compose(dn, after) : after;   // the lanes after t
     uint32_t e = map_apply(G, s_end);
     for (int64_t k = b1 - 1; k >= b0; --k) {
         endst[c * g.nsb + k] = (uint8_t)e;
