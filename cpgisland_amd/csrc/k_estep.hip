@@ -241,30 +241,25 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     const int64_t c = blockIdx.x;
     CPG_EST_MARK(T0)
     const uint32_t* pk = packed + c * (C / 16);
-    if (t < 16) {
-        const int p = t & 3, b = t >> 2;
-        TA[t] = make_double2(model.a[p][b], model.a[p][b + 4]);
-        TB[t] = make_double2(model.a[p + 4][b], model.a[p + 4][b + 4]);
-    }
-    // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4)
+    // the one-step rows from the model's cached table (est_tables: L2-resident, 512 B)
+    // rather than per-lane reads of the kernel-argument model
+    if (t < 32) TA[t] = gtab[t];   // TB = TA + 16
+    const Codes cd0 = lane_codes(pk, t);   // (in flight across the barrier)
+    __syncthreads();
+    // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4), from the rows
     for (int i = t; i < 1024; i += nl) {
-        int b[5];
-#pragma unroll
-        for (int k = 0; k < 5; ++k) b[k] = (i >> (2 * k)) & 3;
         double x00 = 1.0, x01 = 0.0, x10 = 0.0, x11 = 1.0;
 #pragma unroll
         for (int k = 0; k < 4; ++k) {
-            const int p = b[k], q = b[k + 1];
-            const double m00 = model.a[p][q], m01 = model.a[p][q + 4],
-                         m10 = model.a[p + 4][q], m11 = model.a[p + 4][q + 4];
-            const double n00 = x00 * m00 + x01 * m10, n01 = x00 * m01 + x01 * m11;
-            const double n10 = x10 * m00 + x11 * m10, n11 = x10 * m01 + x11 * m11;
+            const int d = (i >> (2 * k)) & 15;   // bases k, k+1 of the window
+            const double2 ma = TA[d], mb = TB[d];
+            const double n00 = x00 * ma.x + x01 * mb.x, n01 = x00 * ma.y + x01 * mb.y;
+            const double n10 = x10 * ma.x + x11 * mb.x, n11 = x10 * ma.y + x11 * mb.y;
             x00 = n00; x01 = n01; x10 = n10; x11 = n11;
         }
         TA4[i] = make_double2(x00, x01);
         TB4[i] = make_double2(x10, x11);
     }
-    const Codes cd0 = lane_codes(pk, t);
     __syncthreads();
     CPG_EST_MARK(T1)
 
