@@ -766,19 +766,15 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     const int cnt = (int)(b1 - b0);
     const bool pre = cnt > 0 && cnt <= kPre;   // cnt == 0: the generic loops do nothing
     // block b0 + i's plan and composites (i < cnt; callers unroll i)
-// (the post composite B is read for SPLIT blocks only: this one workgroup per chunk streams
+// (the post composites are read for SPLIT blocks only: this one workgroup per chunk streams
 // its chunk's block records at one CU's share of the memory system)
-#define CPG_PREFETCH(P, A, B)                                  \
+#define CPG_PREFETCH(P, A)                                     \
     VitPlan P[kPre];                                           \
-    C64 A[kPre], B[kPre];                                      \
+    C64 A[kPre];                                               \
     _Pragma("unroll") for (int i = 0; i < kPre; ++i) {         \
         const int64_t kk = b0 + (i < cnt ? i : 0);             \
         P[i] = pl[kk];                                         \
         A[i] = ld_c64(cp + 2 * kk);                            \
-    }                                                          \
-    _Pragma("unroll") for (int i = 0; i < kPre; ++i) {         \
-        const int64_t kk = b0 + (i < cnt ? i : 0);             \
-        B[i] = P[i].type == PLAN_SPLIT ? ld_c64(cp + 2 * kk + 1) : c64_id(); \
     }
     C64 run = c64_id(), lead = c64_id();
     bool hasb = false;
@@ -795,11 +791,27 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
             run = (p.type == PLAN_SPLIT) ? cb : c64_id();
         }
     };
+    // phase 4 needs, per block, the composite applied after its entry (REGULAR: pre, SPLIT:
+    // post) and the block's kind: kept in LDS from phase 1 (chunks up to 1 Mi) instead of
+    // reading the chunk's records from global memory a second time
+    __shared__ double4 sApp[kPre * kChainT];
+    __shared__ uint8_t sKind[kChainT];   // thread t: 2 bits per block (1 REGULAR, 2 SPLIT)
     if (pre) {
-        CPG_PREFETCH(xp, xa, xb)
+        uint32_t kinds = 0;
+        CPG_PREFETCH(xp, xa)
 #pragma unroll
         for (int i = 0; i < kPre; ++i)
-            if (i < cnt) piece(b0 + i, xp[i], xa[i], xb[i]);
+            if (i < cnt) {
+                const int64_t k = b0 + i;
+                const bool reg = xp[i].type == PLAN_REGULAR, spl = xp[i].type == PLAN_SPLIT;
+                // the post composite: SPLIT blocks only (rare; its load latency stays local)
+                const C64 xb = spl ? ld_c64(cp + 2 * k + 1) : c64_id();
+                piece(k, xp[i], xa[i], xb);
+                sApp[k] = spl ? make_double4(xb.pp, xb.pm, xb.mp, xb.mm)
+                              : make_double4(xa[i].pp, xa[i].pm, xa[i].mp, xa[i].mm);
+                kinds |= (reg ? 1u : spl ? 2u : 0u) << (2 * i);
+            }
+        sKind[t] = (uint8_t)kinds;
     } else {
         for (int64_t k = b0; k < b1; ++k)
             piece(k, pl[k], ld_c64(cp + 2 * k), ld_c64(cp + 2 * k + 1));
@@ -900,7 +912,33 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     }
     __syncthreads();
     CPG_CHAIN_MARK(T3)
-    if (t < 64) {
+    const bool all_staged = nst == nbar && sWoff[nst] <= kStageSteps;
+    if (all_staged) {
+        // every window staged: lane 0 alone runs the chain (no per-window broadcasts)
+        if (t == 0) {
+            double2 v = init;
+            for (int i = 0; i < nbar; ++i) {
+                if (i == 0 && sWk[0] == 0) {   // block 0 (always the first barrier)
+                    v = vhead[c];
+                    voc[0] = v;
+                    continue;
+                }
+                v = c64_apply(v, sGap[i]);
+                double P = v.x, M = v.y;
+                const double4* st = stageL + sWoff[i];
+                const int len = sWb[i] - sWa[i];
+#pragma unroll 8
+                for (int j = 0; j < len; ++j) {
+                    const double4 l = st[j];
+                    const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
+                    P = s.P;
+                    M = s.M;
+                }
+                v = make_double2(P, M);
+                voc[i] = v;
+            }
+        }
+    } else if (t < 64) {
         double2 v = init;
         for (int i = 0; i < nbar; ++i) {
             if (i == 0 && nst > 0 && sWk[0] == 0) {   // block 0 (always the first barrier)
@@ -951,10 +989,22 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         }
     };
     if (pre) {
-        CPG_PREFETCH(xp, xa, xb)
+        const uint32_t kinds = sKind[t];
 #pragma unroll
         for (int i = 0; i < kPre; ++i)
-            if (i < cnt) entries(b0 + i, xp[i], xa[i], xb[i]);
+            if (i < cnt) {
+                const int64_t k = b0 + i;
+                ent[k] = v;
+                const double4 a4 = sApp[k];
+                const C64 ap{a4.x, a4.y, a4.z, a4.w};
+                const uint32_t kd = (kinds >> (2 * i)) & 3u;
+                if (kd == 1u) {
+                    v = c64_apply(v, ap);
+                } else {
+                    v = voc[idx++];
+                    if (kd == 2u) v = c64_apply(v, ap);
+                }
+            }
     } else {
         for (int64_t k = b0; k < b1; ++k)
             entries(k, pl[k], ld_c64(cp + 2 * k), ld_c64(cp + 2 * k + 1));
