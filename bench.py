@@ -142,6 +142,12 @@ def main():
                          "stream), leaving the rest to the decode; 0 = all")
     ap.add_argument("--train-cu-stride", type=int, default=0,
                     help="with --train-cus: leave out every k-th CU instead of the last ones")
+    ap.add_argument("--phase-events", action="store_true",
+                    help="record HIP events around every phase (default: E-step and decode)")
+    ap.add_argument("--decode-event-every", type=int, default=4,
+                    help="record the decode phase's events on every k-th timed step")
+    ap.add_argument("--no-phase-events", action="store_true",
+                    help="(diagnostic) record no per-phase HIP events inside the timed steps")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="write this many MiB of scratch between steps (cold Infinity Cache)")
     args = ap.parse_args()
@@ -200,12 +206,19 @@ def main():
     from cpgisland_amd import baumwelch
     model1 = baumwelch.normalize(ecnt.cpu().numpy())
 
-    names = ("estep", "counts", "reduce", "viterbi", "islands")
+    # HIP events inside the timed steps: the E-step phase (the roofline's dominant kernel) and
+    # the decode phase (on every --decode-event-every-th step) by default; every phase with
+    # --phase-events or --serial.  An event record is not free (a release at the stream's
+    # point of record): 10 per step cost ~9 % of the overlapped throughput, 4 per step ~3 %,
+    # the E-step's 2 per step plus the decode's on every 4th step ~1 %.
+    full_ev = args.phase_events or args.serial
+    names = ("estep", "counts", "reduce", "viterbi", "islands") if full_ev else ("estep", "decode")
     # one pair of HIP events per phase per timed step, read after the final synchronize (no
     # host round trip between steps)
     evs = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
             for k in names} for _ in range(args.steps)]
     acc = {k: 0.0 for k in names}
+    recorded = set()
 
     # The training pass and the decode are independent within a step: by default they run
     # concurrently on two streams (the decode kernels are latency-bound and leave SIMDs idle
@@ -233,8 +246,17 @@ def main():
         cx, s_tr, s_dec = ln["ctx"], ln["s_tr"], ln["s_dec"]
 
         def mark(name, i):
-            if it is not None:
-                evs[it][name][i].record()
+            if it is None or args.no_phase_events:
+                return
+            if full_ev or name == "estep":
+                key = name
+            elif (name, i) in (("viterbi", 0), ("islands", 1)) and it % args.decode_event_every == 0:
+                key, i = "decode", (0 if name == "viterbi" else 1)
+            else:
+                return
+            evs[it][key][i].record()
+            if i == 1:
+                recorded.add((it, key))
         if args.no_overlap or args.serial:
             s_tr.wait_stream(main_s)
             s_dec.wait_stream(main_s)
@@ -282,9 +304,12 @@ def main():
         main_s.wait_stream(ln["s_tr"])
         main_s.wait_stream(ln["s_dec"])
     torch.cuda.synchronize()
-    for ev in evs:
+    nrec = {k: 0 for k in names}
+    for it, ev in enumerate(evs):
         for k, (a, b) in ev.items():
-            acc[k] += a.elapsed_time(b)
+            if (it, k) in recorded:
+                acc[k] += a.elapsed_time(b)
+                nrec[k] += 1
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
@@ -298,7 +323,7 @@ def main():
     steps = args.steps
     ms_per_step = elapsed * 1e3 / steps
     value = N * world * steps / elapsed
-    phases = {k: v / steps for k, v in acc.items()}
+    phases = {k: (v / nrec[k] if nrec[k] else 0.0) for k, v in acc.items()}
     if flush is not None:
         phases_total = sum(phases.values())
         ms_per_step = phases_total   # exclude the cache-flush writes from the step time
@@ -310,7 +335,7 @@ def main():
         # the phase is k_estep_chunk + the ~4 us one-workgroup final kernel).
         dom = "estep"
         alg_bytes = BYTES_PER_BASE[dom] * N
-        ach = alg_bytes / (phases[dom] / 1e3) / 1e9
+        ach = alg_bytes / (phases[dom] / 1e3) / 1e9 if phases[dom] > 0 else 0.0
         roof = {"bound": "hbm", "kernel": "k_estep_chunk", "phase": dom,
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
@@ -321,9 +346,10 @@ def main():
             roof["traffic_source"] = pmc["source"]
         roof["note"] = ("not HBM-bound: LDS/VALU/latency-bound fp64 forward-backward "
                         "(DESIGN.md 5, profiles/*pmc*)")
-        vit = phases["viterbi"] + phases["islands"]
+        vit = phases["viterbi"] + phases["islands"] if full_ev else phases["decode"]
         roof_decode = {"phase": "viterbi+islands", "achieved": round(
-            (BYTES_PER_BASE["viterbi"] + BYTES_PER_BASE["islands"]) * N / (vit / 1e3) / 1e9, 1),
+            (BYTES_PER_BASE["viterbi"] + BYTES_PER_BASE["islands"]) * N / (vit / 1e3) / 1e9
+            if vit > 0 else 0.0, 1),
             "unit": "GB/s", "frac": None}
         roof_decode["frac"] = round(roof_decode["achieved"] / HBM_PEAK_GBS, 4)
         out = {"metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
@@ -337,6 +363,8 @@ def main():
                           "decode_priority": "high" if (args.prio and not args.serial) else "normal",
                           "step_overlap": not (args.no_overlap or args.serial),
                           "pipeline_lanes": nlanes,
+                          "phase_events": ("all" if full_ev else
+                                           f"estep every step, decode every {args.decode_event_every}"),
                           "train_cus": len(tr_cus) if tr_cus else ncu,
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
