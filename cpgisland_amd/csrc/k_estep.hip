@@ -110,6 +110,46 @@ __device__ __forceinline__ Mat mmul_raw(double2 xa, double2 xb, double2 ya, doub
     return {xa.x * ya.x + xa.y * yb.x, xa.x * ya.y + xa.y * yb.y, xb.x * ya.x + xb.y * yb.x,
             xb.x * ya.y + xb.y * yb.y, 0};
 }
+// DPP moves (VALU, no LDS crossbar): CTRL 0x110+n = row_shr:n, 0x100+n = row_shl:n (inside
+// 16-lane rows), 0x138 = wave_shr:1, 0x130 = wave_shl:1.  Lanes without a source take `old`.
+template <int CTRL>
+__device__ __forceinline__ double dpp_f64(double v, double old) {
+    const long long vi = __double_as_longlong(v), oi = __double_as_longlong(old);
+    const int lo = __builtin_amdgcn_update_dpp((int)oi, (int)vi, CTRL, 0xF, 0xF, false);
+    const int hi = __builtin_amdgcn_update_dpp((int)(oi >> 32), (int)(vi >> 32), CTRL, 0xF, 0xF,
+                                               false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+template <int CTRL>
+__device__ __forceinline__ Mat dpp_mat(const Mat& x, const Mat& old) {
+    return {dpp_f64<CTRL>(x.a, old.a), dpp_f64<CTRL>(x.b, old.b), dpp_f64<CTRL>(x.c, old.c),
+            dpp_f64<CTRL>(x.d, old.d),
+            __builtin_amdgcn_update_dpp(old.e, x.e, CTRL, 0xF, 0xF, false)};
+}
+// x from the lane `off` below (up) / above (down) inside its 16-lane row, identity where
+// there is none (off compile-time, < 16): mmul with the identity returns x exactly
+__device__ __forceinline__ Mat row_up(const Mat& x, int off) {
+    const Mat I = {1.0, 0.0, 0.0, 1.0, 0};
+    switch (off) {
+        case 1: return dpp_mat<0x111>(x, I);
+        case 2: return dpp_mat<0x112>(x, I);
+        case 4: return dpp_mat<0x114>(x, I);
+        default: return dpp_mat<0x118>(x, I);
+    }
+}
+__device__ __forceinline__ Mat row_down(const Mat& x, int off) {
+    const Mat I = {1.0, 0.0, 0.0, 1.0, 0};
+    switch (off) {
+        case 1: return dpp_mat<0x101>(x, I);
+        case 2: return dpp_mat<0x102>(x, I);
+        case 4: return dpp_mat<0x104>(x, I);
+        default: return dpp_mat<0x108>(x, I);
+    }
+}
+__device__ __forceinline__ Mat shfl_mat(const Mat& x, int src) {
+    return {__shfl(x.a, src), __shfl(x.b, src), __shfl(x.c, src), __shfl(x.d, src),
+            __shfl(x.e, src)};
+}
 __device__ __forceinline__ Mat shfl_up_mat(const Mat& x, int d) {
     return {__shfl_up(x.a, d), __shfl_up(x.b, d), __shfl_up(x.c, d), __shfl_up(x.d, d),
             __shfl_up(x.e, d)};
@@ -310,13 +350,29 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     const int wv = t >> 6;
     Mat xp = P, xs = P;
 #pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const Mat yp = shfl_up_mat(xp, off), ys = shfl_down_mat(xs, off);
-        const Mat np = mmul(yp, xp), ns = mmul(xs, ys);
-        xp = msel(lane >= off, np, xp);
-        xs = msel(lane + off < 64, ns, xs);
+    for (int off = 1; off < 16; off <<= 1) {   // inside rows: DPP (identity at row edges)
+        const Mat yp = row_up(xp, off), ys = row_down(xs, off);
+        xp = mmul(yp, xp);
+        xs = mmul(xs, ys);
     }
-    const Mat up1 = shfl_up_mat(xp, 1), dn1 = shfl_down_mat(xs, 1);
+    // across rows (the LDS crossbar), the row totals: prefix — rows 1, 3 take the last lane
+    // of the row before, then rows 2, 3 take lane 31; suffix — rows 0, 2 take the first lane
+    // of the row after, then rows 0, 1 take lane 32
+    {
+        const int row = lane >> 4;
+        Mat yp = shfl_mat(xp, (lane | 15) - 16), ys = shfl_mat(xs, (lane & ~15) + 16);
+        Mat np = mmul(yp, xp), ns = mmul(xs, ys);
+        xp = msel(row & 1, np, xp);
+        xs = msel(!(row & 1), ns, xs);
+        yp = shfl_mat(xp, 31);
+        ys = shfl_mat(xs, 32);
+        np = mmul(yp, xp);
+        ns = mmul(xs, ys);
+        xp = msel(row >= 2, np, xp);
+        xs = msel(row < 2, ns, xs);
+    }
+    const Mat I1 = mid();
+    const Mat up1 = dpp_mat<0x138>(xp, I1), dn1 = dpp_mat<0x130>(xs, I1);   // wave_shr/shl:1
     __syncthreads();   // every lane is past its 4-step table reads: the union is free
     Mat* sWP = reinterpret_cast<Mat*>(TA4);   // [16] wave products (prefix order)
     Mat* sWS = sWP + 16;                      // [16] wave products (suffix order)
@@ -328,13 +384,12 @@ __global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
     if (t < 64) {
         Mat wp = t < nw ? sWP[t] : mid(), ws = t < nw ? sWS[t] : mid();
 #pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {
-            const Mat yp = shfl_up_mat(wp, off), ys = shfl_down_mat(ws, off);
-            const Mat np = mmul(yp, wp), ns = mmul(ws, ys);
-            wp = msel(t >= off, np, wp);
-            ws = msel(t + off < 16, ns, ws);
+        for (int off = 1; off < 16; off <<= 1) {   // the 16 wave totals: row 0, DPP
+            const Mat yp = row_up(wp, off), ys = row_down(ws, off);
+            wp = mmul(yp, wp);
+            ws = mmul(ws, ys);
         }
-        const Mat ep = shfl_up_mat(wp, 1), es = shfl_down_mat(ws, 1);
+        const Mat ep = row_up(wp, 1), es = row_down(ws, 1);
         if (t < nw) {
             sXP[t] = t > 0 ? ep : mid();
             sXS[t] = t + 1 < nw ? es : mid();
