@@ -382,6 +382,8 @@ def main():
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     for ln in lanes:
+        if tr_cus:
+            D.cu_stream_destroy(ln["s_tr"])
         ln["ctx"].close()
     if dist:
         torch.distributed.destroy_process_group()

@@ -27,7 +27,8 @@ def _stream():
 
 def cu_stream(device_index: int, cus) -> "torch.cuda.ExternalStream":
     """A stream whose kernels run only on the compute units `cus` (cpg_stream_create_cu),
-    wrapped for torch (events, `torch.cuda.stream(...)`); lives until process exit."""
+    wrapped for torch (events, `torch.cuda.stream(...)`).  Release it with
+    cu_stream_destroy(stream) after its work has completed."""
     ncu = torch.cuda.get_device_properties(device_index).multi_processor_count
     words = np.zeros((ncu + 31) // 32, np.uint32)
     for cu in cus:
@@ -35,6 +36,11 @@ def cu_stream(device_index: int, cus) -> "torch.cuda.ExternalStream":
     h = C.c_void_p()
     check(lib.cpg_stream_create_cu(device_index, ptr(words), len(words), C.byref(h)))
     return torch.cuda.ExternalStream(h.value, device=torch.device("cuda", device_index))
+
+
+def cu_stream_destroy(stream: "torch.cuda.ExternalStream") -> None:
+    stream.synchronize()
+    check(lib.cpg_stream_destroy(C.c_void_p(stream.cuda_stream)))
 
 
 def words16(nbases: int) -> int:
