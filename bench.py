@@ -149,6 +149,10 @@ def main():
                     help="record the decode phase's events on every k-th timed step")
     ap.add_argument("--no-phase-events", action="store_true",
                     help="(diagnostic) record no per-phase HIP events inside the timed steps")
+    ap.add_argument("--decode-split", type=int, default=1,
+                    help="decode each step's chunks as this many independent parts, each on "
+                         "its own context and stream (the per-chunk kernels of the parts "
+                         "overlap)")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="write this many MiB of scratch between steps (cold Infinity Cache)")
     args = ap.parse_args()
@@ -237,6 +241,16 @@ def main():
             tr_cus = list(range(args.train_cus))
     else:
         tr_cus = None
+    nsplit = 1 if (args.serial or ndec < 2) else max(1, min(args.decode_split, ndec))
+    bounds = [ndec * i // nsplit for i in range(nsplit + 1)]   # decode-chunk ranges
+    for ln in lanes:
+        ln["parts"] = []
+        for pi in range(1, nsplit):
+            cx2 = Context(local)
+            cx2.reserve(N)
+            ln["parts"].append({"ctx": cx2, "s": torch.cuda.Stream(priority=-1 if args.prio else 0),
+                                "iout": torch.empty((icap, 32), dtype=torch.uint8, device=dev),
+                                "icnt": torch.zeros(1, dtype=torch.int64, device=dev)})
     for ln in lanes:
         ln["s_tr"] = (main_s if args.serial else
                       D.cu_stream(local, tr_cus) if tr_cus else torch.cuda.Stream())
@@ -263,14 +277,26 @@ def main():
         if args.no_overlap or args.serial:
             s_tr.wait_stream(main_s)
             s_dec.wait_stream(main_s)
-        with torch.cuda.stream(s_dec):
-            mark("viterbi", 0)
-            D.viterbi(cx, model1, dp, N, DECODE, sign_out=ln["so"], score=ln["score"])
-            mark("viterbi", 1)
-            mark("islands", 0)
-            D.islands(cx, dp, ln["so"], N, DECODE, cap=icap, first_chunk=first_chunk,
-                      out=ln["iout"], count=ln["icnt"])
-            mark("islands", 1)
+        # part 0 on the lane's decode stream (chunks [0, bounds[1]); with --decode-split the
+        # other parts on their own streams: independent chunks, so independent calls
+        for pi in range(nsplit - 1, -1, -1):
+            c0, c1 = bounds[pi], bounds[pi + 1]
+            nb = (c1 - c0) * DECODE if pi < nsplit - 1 else N - c0 * DECODE
+            part = ln["parts"][pi - 1] if pi > 0 else None
+            with torch.cuda.stream(part["s"] if part else s_dec):
+                px = part["ctx"] if part else cx
+                if pi == 0:
+                    mark("viterbi", 0)
+                pp, sg = dp[c0 * DECODE // 16:], ln["so"][c0 * DECODE // 32:]
+                D.viterbi(px, model1, pp, nb, DECODE, sign_out=sg, score=ln["score"][c0:])
+                if pi == 0:
+                    mark("viterbi", 1)
+                    mark("islands", 0)
+                D.islands(px, pp, sg, nb, DECODE, cap=icap, first_chunk=first_chunk + c0,
+                          out=part["iout"] if part else ln["iout"],
+                          count=part["icnt"] if part else ln["icnt"])
+                if pi == 0:
+                    mark("islands", 1)
         with torch.cuda.stream(s_tr):
             mark("estep", 0)
             D.bw_estep(cx, model0, dp, N, TRAIN, out=ln["ecnt"])
@@ -306,6 +332,8 @@ def main():
     for ln in lanes:
         main_s.wait_stream(ln["s_tr"])
         main_s.wait_stream(ln["s_dec"])
+        for part in ln["parts"]:
+            main_s.wait_stream(part["s"])
     torch.cuda.synchronize()
     nrec = {k: 0 for k in names}
     for it, ev in enumerate(evs):
@@ -371,7 +399,9 @@ def main():
                           "train_cus": len(tr_cus) if tr_cus else ncu,
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
-                          "islands_found": int(lanes[0]["icnt"].item())},
+                          "decode_parts": nsplit,
+                          "islands_found": int(lanes[0]["icnt"].item()) +
+                                           sum(int(p["icnt"].item()) for p in lanes[0]["parts"])},
                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
                "host_issue_ms_per_step": round(issue * 1e3 / steps, 4),
                "roofline": roof, "roofline_decode": roof_decode}
@@ -384,6 +414,8 @@ def main():
     for ln in lanes:
         if tr_cus:
             D.cu_stream_destroy(ln["s_tr"])
+        for part in ln["parts"]:
+            part["ctx"].close()
         ln["ctx"].close()
     if dist:
         torch.distributed.destroy_process_group()
