@@ -14,7 +14,7 @@
 // (cgCount*islandLen) use Java int arithmetic.
 //
 // Kernels:
-//   T (per tile of 4,096 words = 131,072 positions, all CUs streaming): counts, a workgroup
+//   T (per tile of 1,024 words = 32,768 positions, all CUs streaming): counts, a workgroup
 //     scan, and a record per run boundary with the tile-local prefix counts at it, written
 //     at its tile-local rank into the tile's slice of the run lists; the tile totals;
 //   R (per chunk): tile offsets (scan of the tile totals), per-run stats, stale-atC scan,
@@ -32,7 +32,11 @@ namespace {
 
 constexpr int kIT = 1024;    // lanes of the per-chunk kernels
 constexpr int kTT = 256;     // lanes of the tile kernel
-constexpr int kTRows = 4;    // rows of kTT * 4 words per tile
+#ifndef ISL_TROWS
+#define ISL_TROWS 1
+#endif
+constexpr int kTRows = ISL_TROWS;   // rows of kTT * 4 words per tile (1: 1,376 tiles per
+                                    // 46 Mbp — 7.3 us; 4 rows: 344 tiles — 11.0 us)
 constexpr int64_t kTW = (int64_t)kTT * 4 * kTRows;   // words per tile (4,096)
 
 __device__ __forceinline__ uint32_t compact16(uint32_t x) {   // even bits -> low 16 bits
