@@ -18,12 +18,13 @@
 //     scan, and a record per run boundary with the tile-local prefix counts at it, written
 //     at its tile-local rank into the tile's slice of the run lists; the tile totals;
 //   R (per chunk): tile offsets (scan of the tile totals), per-run stats, stale-atC scan,
-//     filter, kept rank;
-//   D (per chunk): island records at offset = kept islands of earlier chunks.
+//     filter, kept rank, the chunk's first record from a look-back over the earlier chunks'
+//     published counts, island records.
 // A whole chunk per workgroup would stream at one CU's share of the memory system (≈25-70
 // GB/s per CU): the tiles spread the one pass over the data on every CU.
 
 #include <algorithm>
+#include <atomic>
 
 #include "cpg_internal.h"
 
@@ -97,8 +98,7 @@ struct IslWs {
     Cnt5* ttot;         // per tile: totals (kernel T)
     Cnt5* toff;         // per tile: exclusive prefix in its chunk (kernel R)
     int32_t* kept;      // per chunk, maxr: rank*2 | stale_in, or -1
-    int32_t* ncloses;   // per chunk
-    int64_t* nkept;
+    unsigned long long* flags;   // per chunk: epoch << 32 | kept islands (look-back)
     int64_t ntile;      // tiles per chunk
     int64_t cap_t;      // records per tile and kind
     size_t bytes;
@@ -123,8 +123,7 @@ IslWs carve_isl(void* base, int64_t nchunks, int64_t C) {
     w.ttot = (Cnt5*)take(nt * sizeof(Cnt5));
     w.toff = (Cnt5*)take(nt * sizeof(Cnt5));
     w.kept = (int32_t*)take(nchunks * maxr * 4);
-    w.ncloses = (int32_t*)take(nchunks * 4);
-    w.nkept = (int64_t*)take(nchunks * 8);
+    w.flags = (unsigned long long*)take(nchunks * 8);
     w.bytes = o + 256;
     return w;
 }
@@ -396,13 +395,63 @@ __device__ __forceinline__ int32_t wg_scan_sum(const int32_t v, int32_t* sw, int
     return before + x - v;
 }
 
+// where the island records go (the former separate record kernel is fused into R)
+struct IslOut {
+    cpg_island* out;
+    int64_t cap;
+    int64_t* count;            // total records (with base_in)
+    const int64_t* base_in;    // append mode: records already written before this call
+    int64_t first_chunk;
+    uint32_t epoch;            // tags this call's look-back flags
+};
+
+__device__ __forceinline__ void put_island(const IslOut& o, const RunStat& rs, uint32_t stale_in,
+                                           int64_t dst, int64_t gchunk, uint32_t cbase) {
+    if (dst >= o.cap) return;
+    const Rec f = filter(rs, stale_in);
+    cpg_island isl;
+    isl.beg1 = (int32_t)((uint32_t)rs.beg + cbase + 1u);          // :287
+    isl.end1 = (int32_t)((uint32_t)rs.end + cbase + 1u);
+    isl.len = rs.len;
+    isl.chunk = (int32_t)gchunk;
+    isl.cg = f.cg;
+    isl.oe = f.oe;
+    o.out[dst] = isl;
+}
+
+// kept islands of the chunks before c: a look-back over their flags (this call's epoch),
+// one wave, windows of 64 chunks.  Workgroups start in chunk order, so every chunk waited
+// on is running or done; the spin is bounded all the same (2 s of wall clock).
+__device__ __forceinline__ long long kept_before(const IslWs& ws, int64_t c, uint32_t epoch) {
+    const int lane = threadIdx.x & 63;
+    long long sum = 0;
+    const unsigned long long t0 = wall_clock64();
+    for (int64_t j0 = c - 1; j0 >= 0; j0 -= 64) {
+        const int64_t j = j0 - lane;
+        if (j >= 0) {
+            unsigned long long f;
+            for (;;) {
+                f = __hip_atomic_load(ws.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                if ((uint32_t)(f >> 32) == epoch || wall_clock64() - t0 > 200000000ull) break;
+                __builtin_amdgcn_s_sleep(1);
+            }
+            sum += (long long)(uint32_t)f;
+        }
+    }
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
+    return sum;
+}
+
 // the chunk's closed runs split over the lanes: stale-atC maps composed and scanned,
-// filtered (:280-285), kept islands ranked.  With <= 8 runs per lane the map and both filter
-// outcomes (stale 0 / 1) of each run stay in registers: one pass of loads.
+// filtered (:280-285), kept islands ranked, the chunk's first record found by the look-back,
+// records written.  With <= 8 runs per lane the map and both filter outcomes (stale 0 / 1)
+// of each run stay in registers: one pass of loads before the records.
 template <bool kAgent>
 __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws, const Cnt5* to,
-                                             int64_t c, int64_t nr, int32_t* kept, uint32_t* sm,
-                                             int32_t* sk) {
+                                             int64_t c, int64_t C, int64_t nr, int32_t* kept,
+                                             uint32_t* sm, int32_t* sk, long long* sbase,
+                                             const IslOut& o) {
     const int t = threadIdx.x, nl = blockDim.x;
     const int64_t per = (nr + nl - 1) / nl;
     const int64_t r0 = min((int64_t)t * per, nr), r1 = min(r0 + per, nr);
@@ -430,33 +479,49 @@ __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws
     } else {
         for (int64_t r = r0; r < r1; ++r) {
             const RunStat rs = run_stat<kAgent>(pk, ws, to, c, r);
-            const Rec o = filter(rs, stale);
-            kept[r] = o.keep ? (int32_t)stale : -1;   // rank added below
-            nk += o.keep;
+            const Rec f = filter(rs, stale);
+            kept[r] = f.keep ? (int32_t)stale : -1;
+            nk += f.keep;
             stale = mapply(stale_map(rs), stale);
         }
     }
     int32_t nkt;
     int32_t rank = wg_scan_sum(nk, sk, nkt);
+    // publish this chunk's count, then find the kept islands of the chunks before it
+    if (t == 0)
+        __hip_atomic_store(ws.flags + c, ((unsigned long long)o.epoch << 32) | (uint32_t)nkt,
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (t < 64) {
+        const long long before = kept_before(ws, c, o.epoch);
+        if (t == 0) *sbase = before;
+    }
+    __syncthreads();
+    const int64_t base = *sbase + (o.base_in ? *o.base_in : 0);
+    if (c == (int64_t)gridDim.x - 1 && t == 0) *o.count = base + nkt;
+    const int64_t gchunk = o.first_chunk + c;
+    const uint32_t cbase = (uint32_t)gchunk * (uint32_t)C;   // chunk*0x100000, Java int
     if (cached) {
         stale = stale0;
         for (int64_t j = 0; j < r1 - r0; ++j) {
             const uint32_t b = bits >> (4 * j);
-            kept[r0 + j] = ((b >> (2 + stale)) & 1u) ? (int32_t)(((uint32_t)rank++ << 1) | stale) : -1;
+            if ((b >> (2 + stale)) & 1u)
+                put_island(o, run_stat<kAgent>(pk, ws, to, c, r0 + j), stale, base + rank++,
+                           gchunk, cbase);
             stale = mapply(b & 3u, stale);
         }
     } else {
         for (int64_t r = r0; r < r1; ++r)
-            if (kept[r] >= 0) kept[r] |= (rank++) << 1;
+            if (kept[r] >= 0)
+                put_island(o, run_stat<kAgent>(pk, ws, to, c, r), (uint32_t)(kept[r] & 1),
+                           base + rank++, gchunk, cbase);
     }
-    if (t == 0) ws.nkept[c] = nkt;
 }
 
 // R: one chunk.  Tile offsets (exclusive scan of the tile totals, in blocks of kIT tiles;
 // kept in LDS too for up to kToffLds tiles), then resolve_runs.
 constexpr int kToffLds = 1024;
 __global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int64_t C,
-                                                    IslWs ws) {
+                                                    IslWs ws, IslOut o) {
     const int64_t c = blockIdx.x;
     const int t = threadIdx.x, nl = blockDim.x;
     const int64_t maxr = C / 2 + 1;
@@ -464,6 +529,7 @@ __global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int
     __shared__ Cnt5 s5[2][16];
     __shared__ uint32_t sm[16];
     __shared__ int32_t sk[16];
+    __shared__ long long sbase;
     __shared__ Cnt5 s_to[kToffLds];
     const bool in_lds = ws.ntile <= kToffLds;
     Cnt5 carry{0, 0, 0, 0, 0};
@@ -473,9 +539,9 @@ __global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int
         Cnt5 tot;
         const Cnt5 e = wg_scan5(v, s5[it & 1], tot);   // double-buffered: one barrier per block
         if (i < ws.ntile) {
-            const Cnt5 o = cadd(e, carry);
-            ws.toff[c * ws.ntile + i] = o;
-            if (in_lds) s_to[i] = o;
+            const Cnt5 oo = cadd(e, carry);
+            if (in_lds) s_to[i] = oo;
+            else ws.toff[c * ws.ntile + i] = oo;
         }
         carry = cadd(carry, tot);
     }
@@ -483,57 +549,11 @@ __global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int
     __syncthreads();
     // closed runs only: an island still open at the chunk end is dropped (:269-339)
     const int64_t nr = carry.cl;
-    if (t == 0) ws.ncloses[c] = (int32_t)nr;
     int32_t* kept = ws.kept + c * maxr;
     if (in_lds)
-        resolve_runs<false>(pk, ws, s_to, c, nr, kept, sm, sk);
+        resolve_runs<false>(pk, ws, s_to, c, C, nr, kept, sm, sk, &sbase, o);
     else
-        resolve_runs<true>(pk, ws, ws.toff + c * ws.ntile, c, nr, kept, sm, sk);
-}
-
-__global__ __launch_bounds__(kIT) void k_isl_d(const uint32_t* packed, int64_t C,
-                                               int64_t first_chunk, IslWs ws, cpg_island* out,
-                                               int64_t cap, int64_t* count,
-                                               const int64_t* base_in) {
-    const int64_t c = blockIdx.x;
-    // the chunk's first record: kept islands of all earlier chunks (fixed-order sum)
-    __shared__ int64_t sb[kIT];
-    {
-        int64_t a = 0;
-        for (int64_t i = threadIdx.x; i < c; i += kIT) a += ws.nkept[i];
-        sb[threadIdx.x] = a;
-        __syncthreads();
-        for (int o = kIT / 2; o > 0; o >>= 1) {
-            if ((int)threadIdx.x < o) sb[threadIdx.x] += sb[threadIdx.x + o];
-            __syncthreads();
-        }
-    }
-    // append mode (streamed windows): records continue after *base_in earlier ones and
-    // *count receives the running total
-    const int64_t base = sb[0] + (base_in ? *base_in : 0);
-    if (c == (int64_t)gridDim.x - 1 && threadIdx.x == 0) *count = base + ws.nkept[c];
-    const int64_t maxr = C / 2 + 1;
-    const uint32_t* pk = packed + c * (C / 16);
-    const int64_t nr = ws.ncloses[c];
-    const int32_t* kept = ws.kept + c * maxr;
-    const int64_t gchunk = first_chunk + c;
-    const uint32_t cbase = (uint32_t)gchunk * (uint32_t)C;   // chunk*0x100000, Java int
-    for (int64_t r = threadIdx.x; r < nr; r += kIT) {
-        const int32_t k = kept[r];
-        if (k < 0) continue;
-        const int64_t dst = base + (k >> 1);
-        if (dst >= cap) continue;
-        const RunStat rs = run_stat<false>(pk, ws, ws.toff + c * ws.ntile, c, r);
-        const Rec o = filter(rs, (uint32_t)(k & 1));
-        cpg_island isl;
-        isl.beg1 = (int32_t)((uint32_t)rs.beg + cbase + 1u);          // :287
-        isl.end1 = (int32_t)((uint32_t)rs.end + cbase + 1u);
-        isl.len = rs.len;
-        isl.chunk = (int32_t)gchunk;
-        isl.cg = o.cg;
-        isl.oe = o.oe;
-        out[dst] = isl;
-    }
+        resolve_runs<true>(pk, ws, ws.toff + c * ws.ntile, c, C, nr, kept, sm, sk, &sbase, o);
 }
 
 }  // namespace
@@ -553,10 +573,13 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
                        : hipMemsetAsync(count, 0, sizeof(int64_t), s);
     hipLaunchKernelGGL(k_isl_tile, dim3((unsigned)(nchunks * ws.ntile)), dim3(kTT), 0, s, packed,
                        sign, chunk_len, ws);
+    // a fresh tag per call for the look-back flags (stale flags of earlier calls never match)
+    static std::atomic<uint32_t> epoch_ctr{0};
+    uint32_t epoch = ++epoch_ctr;
+    if (epoch == 0) epoch = ++epoch_ctr;
+    const IslOut o{out, cap, count, base_in, first_chunk, epoch};
     hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed,
-                       chunk_len, ws);
-    hipLaunchKernelGGL(k_isl_d, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, chunk_len,
-                       first_chunk, ws, out, cap, count, base_in);
+                       chunk_len, ws, o);
     return hipGetLastError();
 }
 
