@@ -163,10 +163,18 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = world > 1
+    # CPG_BENCH_BACKEND=gloo rehearses the N-rank path on fewer GPUs (ranks share devices,
+    # the reducer's collectives staged through host memory); the measured runs use RCCL
+    backend = os.environ.get("CPG_BENCH_BACKEND", "nccl")
+    if backend != "nccl":
+        local = local % max(1, torch.cuda.device_count())
     if dist:
         os.environ.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
         torch.cuda.set_device(local)
-        torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            torch.distributed.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            torch.distributed.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
 
@@ -400,6 +408,8 @@ def main():
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",
                           "decode_parts": nsplit,
+                          "collectives": (("rccl" if backend == "nccl" else backend)
+                                          if dist else None),
                           "islands_found": int(lanes[0]["icnt"].item()) +
                                            sum(int(p["icnt"].item()) for p in lanes[0]["parts"])},
                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
