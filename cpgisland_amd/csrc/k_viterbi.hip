@@ -1021,6 +1021,37 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
 }
 
 // ---------------------------------------------------------------- K5: re-forward
+__device__ __forceinline__ uint32_t map_apply(uint32_t m, uint32_t x) { return (m >> x) & 1u; }
+__device__ __forceinline__ uint32_t map_compose(uint32_t f, uint32_t g) {   // f o g
+    return map_apply(f, map_apply(g, 0)) | (map_apply(f, map_apply(g, 1)) << 1);
+}
+// w << 1 | c in one VALU op: the compare's lane mask is the carry-in of w + w (the compare
+// writes the mask straight to an SGPR pair; the select + shift-or pair it replaces was two)
+__device__ __forceinline__ uint32_t push_bit(uint32_t w, bool c) {
+    const uint64_t m = __builtin_amdgcn_ballot_w64(c);
+    uint32_t r;
+    uint64_t co;
+    asm("v_addc_co_u32 %0, %1, %2, %2, %3" : "=v"(r), "=s"(co) : "v"(w), "s"(m));
+    return r;
+}
+
+// origin map (bit x = origin sign of the state-x survivor, '+' = 1) of 64 steps from their
+// backpointer bits (bit j of bP / bM: step j's '+' / '-' survivor came from '-'): step j maps
+// its state to the previous one, b_j(1) = !bP_j, b_j(0) = !bM_j, and the quad's map is
+// b_0 o b_1 o ... o b_63 — a 6-level tree of bit-parallel compositions, in the complemented
+// encoding: (f o g).P = g.P ? f.M : f.P, (f o g).M = g.M ? f.M : f.P
+__device__ __forceinline__ uint32_t quad_origin(uint64_t hP, uint64_t hM) {
+#pragma unroll
+    for (int sh = 1; sh < 64; sh <<= 1) {
+        const uint64_t gP = hP >> sh, gM = hM >> sh;
+        const uint64_t nP = (gP & hM) | (~gP & hP);
+        const uint64_t nM = (gM & hM) | (~gM & hP);
+        hP = nP;
+        hM = nM;
+    }
+    return (uint32_t)((~hM & 1u) | ((~hP & 1u) << 1));
+}
+
 __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const uint32_t* packed,
                                                           Geo g, const uint8_t* __restrict__ degen,
                                                           const double2* __restrict__ entry,
@@ -1093,19 +1124,39 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
 #pragma unroll
         for (int j = 0; j < kLook; ++j)
             ring[j] = fetch((j == 0 && k == 0) ? 16u : code(cur, prev, j));
+        uint32_t omap = 0x2u;   // identity
+        uint32_t* o = reinterpret_cast<uint32_t*>(bpo);
 #pragma unroll 1
         for (int q = 0; q < 4; ++q) {
             const uint4 nxt = *reinterpret_cast<const uint4*>(pk + wbase + 4 * (q < 3 ? q + 1 : q));
+            // bits pushed in at the bottom: step jj ends at bit 31 - (jj mod 32), reversed below
+            uint32_t aP0 = 0, aP1 = 0, aM0 = 0, aM1 = 0;
 #pragma unroll
             for (int jj = 0; jj < 64; ++jj) {
                 const C64 l = ring[jj % kLook];
                 const int j2 = jj + kLook;   // past the block's end (q == 3): harmless lookups
                 ring[jj % kLook] = fetch(j2 < 64 ? code(cur, prev, j2) : code(nxt, cur.w, j2 - 64));
-                step2(l.pp, l.pm, l.mp, l.mm, q, jj);
+                const Step st = ref_step(P, M, l.pp, l.pm, l.mp, l.mm);
+                P = st.P;
+                M = st.M;
+                if (jj < 32) {
+                    aP0 = push_bit(aP0, st.bP);
+                    aM0 = push_bit(aM0, st.bM);
+                } else {
+                    aP1 = push_bit(aP1, st.bP);
+                    aM1 = push_bit(aM1, st.bM);
+                }
             }
+            const uint32_t p0 = __builtin_bitreverse32(aP0), p1 = __builtin_bitreverse32(aP1);
+            const uint32_t m0 = __builtin_bitreverse32(aM0), m1 = __builtin_bitreverse32(aM1);
+            o[2 * q] = p0; o[2 * q + 1] = p1; o[8 + 2 * q] = m0; o[8 + 2 * q + 1] = m1;
+            omap = map_compose(omap, quad_origin(p0 | ((uint64_t)p1 << 32),
+                                                 m0 | ((uint64_t)m1 << 32)));
             prev = cur.w;
             cur = nxt;
         }
+        oP = (omap >> 1) & 1u;
+        oM = omap & 1u;
     } else {
         // partial/first block: positions outside the chunk are skipped; flush every quad
         walk_block<false>(pk, k, g.C, [&](uint32_t d, int q, int jj) {
@@ -1130,10 +1181,6 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
 }
 
 // ---------------------------------------------------------------- K6: trace scan
-__device__ __forceinline__ uint32_t map_apply(uint32_t m, uint32_t x) { return (m >> x) & 1u; }
-__device__ __forceinline__ uint32_t map_compose(uint32_t f, uint32_t g) {   // f o g
-    return map_apply(f, map_apply(g, 0)) | (map_apply(f, map_apply(g, 1)) << 1);
-}
 
 __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __restrict__ entry,
                                                         const uint8_t* __restrict__ origin,
