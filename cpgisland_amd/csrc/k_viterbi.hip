@@ -792,12 +792,20 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         }
     };
     // phase 4 needs, per block, the composite applied after its entry (REGULAR: pre, SPLIT:
-    // post) and the block's kind: kept in LDS from phase 1 (chunks up to 1 Mi) instead of
-    // reading the chunk's records from global memory a second time
+    // post) and the block's kind: kept in LDS and a register from phase 1 (chunks up to 1 Mi)
+    // instead of reading the chunk's records from global memory a second time
     __shared__ double4 sApp[kPre * kChainT];
-    __shared__ uint8_t sKind[kChainT];   // thread t: 2 bits per block (1 REGULAR, 2 SPLIT)
+    uint32_t kinds = 0;   // 2 bits per block of the thread (1 REGULAR, 2 SPLIT, 3 SEQ)
+    uint32_t wab[kPre] = {};   // barrier blocks' window [ja, jb) as ja | jb << 16
+    // phase 3's staging metadata (first kMaxStagedBar barriers), written by phase 2's list
+    // loop straight from registers when every thread's blocks were prefetched (chunks up to
+    // 1 Mi): no global round trip through the barrier list and the plans before the chain
+    __shared__ int sWoff[kMaxStagedBar + 1];
+    __shared__ int sWa[kMaxStagedBar], sWb[kMaxStagedBar];
+    __shared__ int64_t sWk[kMaxStagedBar];
+    __shared__ C64 sGap[kMaxStagedBar];
+    const bool pre_all = per <= kPre;   // uniform: every thread with blocks prefetched them
     if (pre) {
-        uint32_t kinds = 0;
         CPG_PREFETCH(xp, xa)
 #pragma unroll
         for (int i = 0; i < kPre; ++i)
@@ -809,9 +817,11 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
                 piece(k, xp[i], xa[i], xb);
                 sApp[k] = spl ? make_double4(xb.pp, xb.pm, xb.mp, xb.mm)
                               : make_double4(xa[i].pp, xa[i].pm, xa[i].mp, xa[i].mm);
-                kinds |= (reg ? 1u : spl ? 2u : 0u) << (2 * i);
+                const bool seq = xp[i].type == PLAN_SEQ;
+                kinds |= (reg ? 1u : spl ? 2u : seq ? 3u : 0u) << (2 * i);
+                const uint32_t ja = spl ? xp[i].t1 : g.jfirst(k), jb = spl ? xp[i].t2 : g.jend(k);
+                wab[i] = k == 0 ? 0u : (ja | (jb << 16));   // block 0: walked by K1's head lanes
             }
-        sKind[t] = (uint8_t)kinds;
     } else {
         for (int64_t k = b0; k < b1; ++k)
             piece(k, pl[k], ld_c64(cp + 2 * k), ld_c64(cp + 2 * k + 1));
@@ -852,7 +862,27 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     const int bidx0 = excl.n;
     int nbar = 0;
     for (int w = 0; w < kChainT / 64; ++w) nbar += sWave[w].n;
-    {
+    if (pre) {   // the kinds from phase 1: no second read of the plans
+        int idx = bidx0;
+        bool first = true;
+#pragma unroll
+        for (int i = 0; i < kPre; ++i) {
+            const int64_t k = b0 + i;
+            if (i < cnt && ((kinds >> (2 * i)) & 3u) >= 2u) {
+                const C64 gp = first ? c64_mul(incoming, lead) : ld_c64(gkc + k);
+                blc[idx] = (int32_t)k;
+                st_c64(gpc + idx, gp);
+                if (idx < kMaxStagedBar) {
+                    sWk[idx] = k;
+                    sWa[idx] = (int)(wab[i] & 0xFFFFu);
+                    sWb[idx] = (int)(wab[i] >> 16);
+                    sGap[idx] = gp;
+                }
+                first = false;
+                ++idx;
+            }
+        }
+    } else {
         int idx = bidx0;
         bool first = true;
         for (int64_t k = b0; k < b1; ++k) {
@@ -875,12 +905,8 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     // back to per-window staging by wave 0.
     const uint32_t o0 = base_at(pk, 0);
     const double2 init = make_double2(vc.logpi[o0], vc.logpi[o0 + 4]);
-    __shared__ int sWoff[kMaxStagedBar + 1];
-    __shared__ int sWa[kMaxStagedBar], sWb[kMaxStagedBar];
-    __shared__ int64_t sWk[kMaxStagedBar];
-    __shared__ C64 sGap[kMaxStagedBar];
     const int nst = min(nbar, kMaxStagedBar);
-    if (t < nst) {
+    if (!pre_all && t < nst) {
         const int64_t k = blc[t];
         const VitPlan p = pl[k];
         sWk[t] = k;
@@ -989,7 +1015,6 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         }
     };
     if (pre) {
-        const uint32_t kinds = sKind[t];
 #pragma unroll
         for (int i = 0; i < kPre; ++i)
             if (i < cnt) {
@@ -1013,10 +1038,11 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     CPG_CHAIN_MARK(T5)
 #ifdef CPG_DEBUG_CHAIN
     if (t == 0 && (c == 0 || c == g.nchunks - 1))
-        printf("chain c%lld nbar %d: phase1 %llu scan %llu (shfl %llu bar1 %llu combine+list %llu "
-               "bar2 %llu) list+stage %llu serial %llu entries %llu (wall-clock ticks)\n",
-               (long long)c, nbar, T1 - T0, T2 - T1, T1a - T1, T1b - T1a, T1c - T1b, T2 - T1c,
-               T3 - T2, T4 - T3, T5 - T4);
+        printf("chain c%lld nbar %d steps %d staged %d: phase1 %llu scan %llu (shfl %llu bar1 %llu "
+               "combine+list %llu bar2 %llu) list+stage %llu serial %llu entries %llu "
+               "(wall-clock ticks)\n",
+               (long long)c, nbar, sWoff[nst], (int)all_staged, T1 - T0, T2 - T1, T1a - T1,
+               T1b - T1a, T1c - T1b, T2 - T1c, T3 - T2, T4 - T3, T5 - T4);
 #endif
 }
 
