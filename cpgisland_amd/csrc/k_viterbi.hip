@@ -759,6 +759,9 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     int32_t* blc = barlist + c * g.nsb;
     double2* voc = vout + c * g.nsb;
 
+    // block 0's exit value (K1's head lanes), needed by the serial chain: read now, so that its
+    // latency is not on the chain
+    const double2 vhead0 = t == 0 ? vhead[c] : make_double2(0.0, 0.0);
     CPG_CHAIN_MARK(T0)
     // phase 1: thread-local pieces.  A thread owns `per` (<= kPre for chunks up to 1 Mi)
     // consecutive blocks; their plans and composites are loaded up front, all in flight.
@@ -940,19 +943,34 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     CPG_CHAIN_MARK(T3)
     const bool all_staged = nst == nbar && sWoff[nst] <= kStageSteps;
     if (all_staged) {
-        // every window staged: lane 0 alone runs the chain (no per-window broadcasts)
+        // every window staged: lane 0 alone runs the chain (no per-window broadcasts); the
+        // next window's offset, length and gap are read while this one's steps run
         if (t == 0) {
             double2 v = init;
-            for (int i = 0; i < nbar; ++i) {
-                if (i == 0 && sWk[0] == 0) {   // block 0 (always the first barrier)
-                    v = vhead[c];
-                    voc[0] = v;
-                    continue;
+            int i0 = 0;
+            if (nbar > 0 && sWk[0] == 0) {   // block 0 (always the first barrier)
+                v = vhead0;
+                voc[0] = v;
+                i0 = 1;
+            }
+            int offn = 0, lenn = 0;
+            C64 gapn = c64_id();
+            if (i0 < nbar) {
+                offn = sWoff[i0];
+                lenn = sWb[i0] - sWa[i0];
+                gapn = sGap[i0];
+            }
+            for (int i = i0; i < nbar; ++i) {
+                const int off = offn, len = lenn;
+                const C64 gp = gapn;
+                if (i + 1 < nbar) {
+                    offn = sWoff[i + 1];
+                    lenn = sWb[i + 1] - sWa[i + 1];
+                    gapn = sGap[i + 1];
                 }
-                v = c64_apply(v, sGap[i]);
+                v = c64_apply(v, gp);
                 double P = v.x, M = v.y;
-                const double4* st = stageL + sWoff[i];
-                const int len = sWb[i] - sWa[i];
+                const double4* st = stageL + off;
 #pragma unroll 8
                 for (int j = 0; j < len; ++j) {
                     const double4 l = st[j];
