@@ -437,7 +437,9 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
 }
 
 // ---------------------------------------------------------------- K3: exact composites
-// comp3 per block: pre (4 doubles) | post (4 doubles)
+// comp3: the pre composites of all blocks [nchunks * nsb], then the post composites [same];
+// a block's post is written (and read) for SPLIT blocks only, so K4's one workgroup per chunk
+// streams dense pre records, not every other 32 B of a 64-B pair
 // largest finite magnitude (the identity's -inf entries carry no rounding)
 __device__ __forceinline__ double fin(double x) { return x > -INFINITY ? fabs(x) : 0.0; }
 __device__ __forceinline__ double c64_absmax(const C64& c) {
@@ -525,8 +527,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
         plan[gid].type = PLAN_SEQ;   // exactness not guaranteed: let K4 run it sequentially
         return;
     }
-    comp3[gid * 2] = make_double4(acc.pp, acc.pm, acc.mp, acc.mm);
-    comp3[gid * 2 + 1] = make_double4(0.0, -INFINITY, -INFINITY, 0.0);
+    comp3[gid] = make_double4(acc.pp, acc.pm, acc.mp, acc.mm);
 }
 
 // K3b: irregular blocks, 16 lanes per block (lane i owns positions [16i, 16i+16)):
@@ -675,8 +676,8 @@ __device__ void vit_irregular(const VitConsts& vc, const uint32_t* packed, const
             if (exact) {
                 plan[gid] = VitPlan{PLAN_SPLIT, (int8_t)e, (int8_t)(e + 1), 0, (uint16_t)t1,
                                     (uint16_t)t2};
-                comp3[gid * 2] = make_double4(pre.pp, pre.pm, pre.mp, pre.mm);
-                comp3[gid * 2 + 1] = make_double4(post.pp, post.pm, post.mp, post.mm);
+                comp3[gid] = make_double4(pre.pp, pre.pm, pre.mp, pre.mm);
+                comp3[g.nchunks * g.nsb + gid] = make_double4(post.pp, post.pm, post.mp, post.mm);
             } else {
                 plan[gid] = VitPlan{PLAN_SEQ, 0, 0, 0, 0, 0};
             }
@@ -753,7 +754,8 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     }
     const uint32_t* pk = chunk_ptr(packed, g, c);
     const VitPlan* pl = plan + c * g.nsb;
-    const double4* cp = comp3 + c * g.nsb * 2;
+    const double4* cp = comp3 + c * g.nsb;                          // pre composites
+    const double4* cq = comp3 + (g.nchunks + c) * g.nsb;            // post (SPLIT only)
     double4* gkc = gk + c * g.nsb;
     double4* gpc = gap + c * g.nsb;
     int32_t* blc = barlist + c * g.nsb;
@@ -777,7 +779,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     _Pragma("unroll") for (int i = 0; i < kPre; ++i) {         \
         const int64_t kk = b0 + (i < cnt ? i : 0);             \
         P[i] = pl[kk];                                         \
-        A[i] = ld_c64(cp + 2 * kk);                            \
+        A[i] = ld_c64(cp + kk);                                \
     }
     C64 run = c64_id(), lead = c64_id();
     bool hasb = false;
@@ -816,7 +818,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
                 const int64_t k = b0 + i;
                 const bool reg = xp[i].type == PLAN_REGULAR, spl = xp[i].type == PLAN_SPLIT;
                 // the post composite: SPLIT blocks only (rare; its load latency stays local)
-                const C64 xb = spl ? ld_c64(cp + 2 * k + 1) : c64_id();
+                const C64 xb = spl ? ld_c64(cq + k) : c64_id();
                 piece(k, xp[i], xa[i], xb);
                 sApp[k] = spl ? make_double4(xb.pp, xb.pm, xb.mp, xb.mm)
                               : make_double4(xa[i].pp, xa[i].pm, xa[i].mp, xa[i].mm);
@@ -827,7 +829,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
             }
     } else {
         for (int64_t k = b0; k < b1; ++k)
-            piece(k, pl[k], ld_c64(cp + 2 * k), ld_c64(cp + 2 * k + 1));
+            piece(k, pl[k], ld_c64(cp + k), ld_c64(cq + k));
     }
     if (!hasb) lead = run;
     CPG_CHAIN_MARK(T1)
@@ -1050,7 +1052,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
             }
     } else {
         for (int64_t k = b0; k < b1; ++k)
-            entries(k, pl[k], ld_c64(cp + 2 * k), ld_c64(cp + 2 * k + 1));
+            entries(k, pl[k], ld_c64(cp + k), ld_c64(cq + k));
     }
     if (b1 == g.nsb && b0 < b1) ent[g.nsb] = v;
     CPG_CHAIN_MARK(T5)
@@ -1117,9 +1119,12 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
-    uint4* bpo = bp + gid * 4;   // words 0..7 bpP, 8..15 bpM
+    // backpointers quad-major: bp[q * nt + gid] = {bP bits 0-31, 32-63, bM bits 0-31, 32-63} of
+    // the block's quad q (64 steps), so that each quad's store is one coalesced 16-B/lane row
+    const int64_t nt = g.nchunks * g.nsb;
+    uint4* bpo = bp + gid;
     if (degen[c]) {
-        for (int i = 0; i < 4; ++i) bpo[i] = make_uint4(0, 0, 0, 0);
+        for (int i = 0; i < 4; ++i) bpo[i * nt] = make_uint4(0, 0, 0, 0);
         origin[gid] = 0x2;   // identity
         return;
     }
@@ -1130,8 +1135,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
     uint32_t oP = 1u, oM = 0u;   // origin sign of the current '+' / '-' survivor
     uint32_t wP0 = 0, wP1 = 0, wM0 = 0, wM1 = 0;
     auto flush = [&](int q) {
-        uint32_t* o = reinterpret_cast<uint32_t*>(bpo);
-        o[2 * q] = wP0; o[2 * q + 1] = wP1; o[8 + 2 * q] = wM0; o[8 + 2 * q + 1] = wM1;
+        bpo[q * nt] = make_uint4(wP0, wP1, wM0, wM1);
         wP0 = wP1 = wM0 = wM1 = 0;
     };
     auto step2 = [&](double l0, double l1, double l2, double l3, int q, int jj) {
@@ -1169,7 +1173,6 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
         for (int j = 0; j < kLook; ++j)
             ring[j] = fetch((j == 0 && k == 0) ? 16u : code(cur, prev, j));
         uint32_t omap = 0x2u;   // identity
-        uint32_t* o = reinterpret_cast<uint32_t*>(bpo);
 #pragma unroll 1
         for (int q = 0; q < 4; ++q) {
             const uint4 nxt = *reinterpret_cast<const uint4*>(pk + wbase + 4 * (q < 3 ? q + 1 : q));
@@ -1193,7 +1196,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
             }
             const uint32_t p0 = __builtin_bitreverse32(aP0), p1 = __builtin_bitreverse32(aP1);
             const uint32_t m0 = __builtin_bitreverse32(aM0), m1 = __builtin_bitreverse32(aM1);
-            o[2 * q] = p0; o[2 * q + 1] = p1; o[8 + 2 * q] = m0; o[8 + 2 * q + 1] = m1;
+            bpo[q * nt] = make_uint4(p0, p1, m0, m1);
             omap = map_compose(omap, quad_origin(p0 | ((uint64_t)p1 << 32),
                                                  m0 | ((uint64_t)m1 << 32)));
             prev = cur.w;
@@ -1208,11 +1211,10 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
         });
         // quads whose last position was skipped were not flushed: flush all remaining
         const int jend = g.jend(k);
-        uint32_t* o = reinterpret_cast<uint32_t*>(bpo);
         for (int q = 0; q < 4; ++q) {
             const int last = q * 64 + 63;
             if (last >= jend) {
-                o[2 * q] = wP0; o[2 * q + 1] = wP1; o[8 + 2 * q] = wM0; o[8 + 2 * q + 1] = wM1;
+                bpo[q * nt] = make_uint4(wP0, wP1, wM0, wM1);
                 wP0 = wP1 = wM0 = wM1 = 0;
             }
         }
@@ -1275,12 +1277,13 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     uint32_t wP[8], wM[8];
     {
-        const uint4* b = bp + gid * 4;
-        uint4 x0 = b[0], x1 = b[1], x2 = b[2], x3 = b[3];
-        wP[0] = x0.x; wP[1] = x0.y; wP[2] = x0.z; wP[3] = x0.w;
-        wP[4] = x1.x; wP[5] = x1.y; wP[6] = x1.z; wP[7] = x1.w;
-        wM[0] = x2.x; wM[1] = x2.y; wM[2] = x2.z; wM[3] = x2.w;
-        wM[4] = x3.x; wM[5] = x3.y; wM[6] = x3.z; wM[7] = x3.w;
+        const int64_t nt = g.nchunks * g.nsb;   // quad-major layout (k_vit_forward)
+        const uint4* b = bp + gid;
+        const uint4 x0 = b[0], x1 = b[nt], x2 = b[2 * nt], x3 = b[3 * nt];
+        wP[0] = x0.x; wP[1] = x0.y; wM[0] = x0.z; wM[1] = x0.w;
+        wP[2] = x1.x; wP[3] = x1.y; wM[2] = x1.z; wM[3] = x1.w;
+        wP[4] = x2.x; wP[5] = x2.y; wM[4] = x2.z; wM[5] = x2.w;
+        wP[6] = x3.x; wP[7] = x3.y; wM[6] = x3.z; wM[7] = x3.w;
     }
     // Word-parallel traceback.  Position j's backpointers are a map m_j: state at j ->
     // state at j-1 (m_j(+) = ~bP_j, m_j(-) = ~bM_j; identity past the block's end).  The
