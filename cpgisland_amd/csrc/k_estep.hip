@@ -256,7 +256,13 @@ __device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int
 #else
 #define CPG_EST_MARK(n)
 #endif
-__global__ __launch_bounds__(kET) void k_estep_chunk(const cpg_model model,
+// waves per SIMD: 4 (123 VGPRs, no spills).  5 (<= 96 VGPRs, 23 spilled) was measured so that
+// decode waves could share the training CUs: 208 vs 218-224 Gbase/s (r01_v10 A/B), rejected.
+#ifndef CPG_EST_WPE
+#define CPG_EST_WPE 4
+#endif
+__global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(CPG_EST_WPE)))
+void k_estep_chunk(const cpg_model model,
                                                      const uint32_t* __restrict__ packed,
                                                      int64_t C,
                                                      unsigned long long* __restrict__ acc,
