@@ -59,7 +59,8 @@ hipStream_t pick(cpg_ctx*, void* stream) { return static_cast<hipStream_t>(strea
 bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15u) == 0; }
 
 // device copy of the per-binade tables of one model (model-only; cached per context)
-int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitTables** out) {
+int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitConsts& vc, const VitTables& vt,
+               const VitTables** out) {
     for (int i = 0; i < ctx->vtn; ++i)
         if (std::memcmp(&ctx->vtc[i].model, m, sizeof *m) == 0) {
             *out = ctx->vtc[i].d;
@@ -68,14 +69,19 @@ int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitT
     cpg_ctx::VtSlot* sl;
     if (ctx->vtn < cpg_ctx::kVtSlots) {
         sl = &ctx->vtc[ctx->vtn++];
-        CPG_HIP(hipMalloc(&sl->d, sizeof(VitTables)));
+        CPG_HIP(hipMalloc(&sl->d, sizeof(VitTables) + vit_derived_bytes()));
     } else {
         sl = &ctx->vtc[ctx->vtnext];
         ctx->vtnext = (ctx->vtnext + 1) % cpg_ctx::kVtSlots;
         CPG_HIP(hipDeviceSynchronize());   // the evicted slot may still be read
     }
-    sl->model = *m;
+    std::memset(&sl->model, 0xFF, sizeof sl->model);   // NaN bytes: no model matches a half-built slot
     CPG_HIP(hipMemcpy(sl->d, &vt, sizeof(VitTables), hipMemcpyHostToDevice));
+    // K1's 4-step and K3's per-binade tables, computed once here instead of by every
+    // workgroup of every call (they depend on the model only: qshift and Le do)
+    CPG_HIP(launch_vit_tables(vc, sl->d, nullptr));
+    CPG_HIP(hipStreamSynchronize(nullptr));
+    sl->model = *m;
     *out = sl->d;
     return CPG_OK;
 }
@@ -267,7 +273,7 @@ int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed
     static thread_local VitTables vt;
     if ((rc = vit_prepare(model, chunk_len, &vc, &vt))) return rc;
     const VitTables* d_vt;
-    if ((rc = vit_tables(ctx, model, vt, &d_vt))) return rc;
+    if ((rc = vit_tables(ctx, model, vc, vt, &d_vt))) return rc;
     void* ws;
     const size_t need = viterbi_ws_bytes(nch, chunk_len);
     if ((rc = ws_get(ctx, WS_VIT, need, &ws))) return rc;

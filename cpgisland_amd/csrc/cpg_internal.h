@@ -103,7 +103,8 @@ int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out);
 int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out);
 int model_check_deterministic(const cpg_model* m);
 bool aligned16(const void* p);
-int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitTables& vt, const VitTables** out);
+int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitConsts& vc, const VitTables& vt,
+               const VitTables** out);
 int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out);
 enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
        WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9, WS_GEN = 10, WS_GISL = 11, WS_CSORT = 12,
@@ -125,6 +126,9 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                           uint32_t* status, hipStream_t s, uint32_t* zero_at = nullptr,
                           int64_t zero_n = 0);
 size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len);
+// model-derived LDS tables of K1/K3, built once per model right after the VitTables copy
+size_t vit_derived_bytes();
+hipError_t launch_vit_tables(const VitConsts& vc, VitTables* d_vt, hipStream_t s);
 int64_t vit_nsb(int64_t chunk_len);
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* ws, size_t ws_bytes,

@@ -111,7 +111,7 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
     const VitTables* d_vt = nullptr;
     if (decode) {
         if ((rc = vit_prepare(decode_model, D, &vc, &vt))) return rc;
-        if ((rc = vit_tables(ctx, decode_model, vt, &d_vt))) return rc;
+        if ((rc = vit_tables(ctx, decode_model, vc, vt, &d_vt))) return rc;
     }
     // workspaces sized for the largest window up front (ws_get may reallocate)
     void *ws_cnt = nullptr, *ws_vit = nullptr, *ws_isl = nullptr, *ws_est = nullptr;

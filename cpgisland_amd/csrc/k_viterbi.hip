@@ -266,8 +266,57 @@ __device__ void vit_head(const VitConsts& vc, const uint32_t* packed, const Geo&
     vhead[c] = make_double2(P, M);
 }
 
+// ---------------------------------------------------------------- model-derived tables
+// K1's 4-step fixed-point products and K3's per-binade step / 2-step tables depend on the
+// model only; k_vit_tables writes them once per model (vit_tables' cache) right after the
+// VitTables in the same allocation, and every K1/K3 workgroup copies its part to LDS.
+constexpr int kQ4 = 1280;   // 4-step products over 5-base windows [0, 1024), 3-step [1024, 1280)
+struct VitDerived {
+    int4 Q4[kQ4];
+    double2 sA[kMaxBinade * 16], sB[kMaxBinade * 16];    // single-step halves (l0,l1) | (l2,l3)
+    double2 P2A[kMaxBinade * 64], P2B[kMaxBinade * 64];  // 2-step composites (pp,pm) | (mp,mm)
+};
+__device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
+    return reinterpret_cast<const VitDerived*>(vt + 1);
+}
+
+__global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables* vt) {
+    VitDerived* dv = reinterpret_cast<VitDerived*>(vt + 1);
+    const int n = kQ4 + kMaxBinade * 16 + kMaxBinade * 64;
+    for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
+        if (i < kQ4) {   // i >= 1024: 3-step entries (block 0's first window; b0 unused)
+            const bool three = i >= 1024;
+            const int w = three ? (i - 1024) << 2 : i;
+            auto qd = [&](int d) {
+                return q_mat(make_int4(vc.Q[d][0], vc.Q[d][1], vc.Q[d][2], vc.Q[d][3]));
+            };
+            int4 m = three ? make_int4(0, kNeg32, kNeg32, 0) : qd((w & 3) | (((w >> 2) & 3) << 2));
+            for (int k = 1; k < 4; ++k) {
+                const int p = (w >> (2 * k)) & 3, b = (w >> (2 * k + 2)) & 3;
+                m = i4_mul(m, qd(p | (b << 2)));
+            }
+            dv->Q4[i] = m;
+        } else if (i < kQ4 + kMaxBinade * 16) {
+            const int j = i - kQ4;
+            const double* l = vt->Le[j / 16][j % 16];
+            dv->sA[j] = make_double2(l[0], l[1]);
+            dv->sB[j] = make_double2(l[2], l[3]);
+        } else {
+            const int j = i - kQ4 - kMaxBinade * 16, e = j / 64, w = j % 64;
+            const double* l1 = vt->Le[e][(w & 3) | (((w >> 2) & 3) << 2)];          // x -> y
+            const double* l2 = vt->Le[e][((w >> 2) & 3) | (((w >> 4) & 3) << 2)];   // y -> z
+            // composite of one step: (pp, pm, mp, mm) = (l0, l2, l1, l3)
+            C64 m{l1[0], l1[2], l1[1], l1[3]};
+            c64_step(m, l2[0], l2[1], l2[2], l2[3]);
+            dv->P2A[j] = make_double2(m.pp, m.pm);
+            dv->P2B[j] = make_double2(m.mp, m.mm);
+        }
+    }
+}
+
 __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uint32_t* packed,
-                                                         Geo g, int4* __restrict__ comp,
+                                                         Geo g, const VitTables* vt,
+                                                         int4* __restrict__ comp,
                                                          unsigned main_grid,
                                                          double2* __restrict__ vhead) {
     if (blockIdx.x >= main_grid) {   // workgroup-uniform: head workgroups
@@ -278,37 +327,19 @@ __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uin
     __shared__ int4 Q[16];
     // 4-step products over 5-base windows b0..b4 (exact: integers) [0, 1024), then the
     // 3-step products of steps 1..3 over b1..b4 [1024, 1280): block 0's first window (the
-    // chunk's position 0 carries no step)
-    __shared__ int4 Q4[1280];
+    // chunk's position 0 carries no step) — copied from the per-model tables (k_vit_tables)
+    __shared__ int4 Q4[kQ4];
     if (threadIdx.x < 16)
         Q[threadIdx.x] = make_int4(vc.Q[threadIdx.x][0], vc.Q[threadIdx.x][1],
                                    vc.Q[threadIdx.x][2], vc.Q[threadIdx.x][3]);
-    __syncthreads();
-#ifndef VIT_ABL_K1   // development ablations (tools/build_ablations.sh); product: undefined
-#define VIT_ABL_K1 0
-#endif
-    for (int i = threadIdx.x; i < 1280; i += kThreads) {
-        if (VIT_ABL_K1 == 1) { Q4[i] = make_int4(i, -i, 3 * i, i >> 2); continue; }
-        const bool three = i >= 1024;
-        const int w = three ? (i - 1024) << 2 : i;   // b0 = 0 unused for the 3-step entries
-        int4 m = three ? make_int4(0, kNeg32, kNeg32, 0)
-                       : q_mat(Q[(w & 3) | (((w >> 2) & 3) << 2)]);
+    const int4* gq = derived(vt)->Q4;
 #pragma unroll
-        for (int k = 1; k < 4; ++k) {
-            const int p = (w >> (2 * k)) & 3, b = (w >> (2 * k + 2)) & 3;
-            m = i4_mul(m, q_mat(Q[p | (b << 2)]));
-        }
-        Q4[i] = m;
-    }
+    for (int i = 0; i < kQ4 / kThreads; ++i) Q4[threadIdx.x + i * kThreads] = gq[threadIdx.x + i * kThreads];
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     const uint32_t* pk = chunk_ptr(packed, g, c);
-    if (VIT_ABL_K1 == 2) {
-        comp[gid] = Q4[gid & 1023];
-        return;
-    }
     if (g.whole(k)) {
         int4 acc = make_int4(0, kNeg32, kNeg32, 0);
         const BlockWords bw = load_block(pk, k);
@@ -473,20 +504,16 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     double2* sB = sA + nb * 16;
     double2* P2A = sB + nb * 16;
     double2* P2B = P2A + nb * 64;
-    for (int i = threadIdx.x; i < nb * 16; i += kThreads) {
-        const double* s = vt->Le[vc.emin + i / 16][i % 16];
-        sA[i] = make_double2(s[0], s[1]);
-        sB[i] = make_double2(s[2], s[3]);
-    }
-    for (int i = threadIdx.x; i < nb * 64; i += kThreads) {
-        const int e = vc.emin + i / 64, w = i % 64;
-        const double* l1 = vt->Le[e][(w & 3) | (((w >> 2) & 3) << 2)];          // x -> y
-        const double* l2 = vt->Le[e][((w >> 2) & 3) | (((w >> 4) & 3) << 2)];   // y -> z
-        // composite of one step: (pp, pm, mp, mm) = (l0, l2, l1, l3)
-        C64 m{l1[0], l1[2], l1[1], l1[3]};
-        c64_step(m, l2[0], l2[1], l2[2], l2[3]);
-        P2A[i] = make_double2(m.pp, m.pm);
-        P2B[i] = make_double2(m.mp, m.mm);
+    {   // the binades [emin, emax] of the per-model tables (k_vit_tables)
+        const VitDerived* dv = derived(vt);
+        for (int i = threadIdx.x; i < nb * 16; i += kThreads) {
+            sA[i] = dv->sA[vc.emin * 16 + i];
+            sB[i] = dv->sB[vc.emin * 16 + i];
+        }
+        for (int i = threadIdx.x; i < nb * 64; i += kThreads) {
+            P2A[i] = dv->P2A[vc.emin * 64 + i];
+            P2B[i] = dv->P2B[vc.emin * 64 + i];
+        }
     }
     __syncthreads();
     if (blockIdx.x >= main_grid) {   // workgroup-uniform: the chunk's irregular blocks
@@ -1400,7 +1427,7 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     const unsigned grid = (unsigned)((nt + kThreads - 1) / kThreads);
     const unsigned head = (unsigned)((nchunks + kThreads - 1) / kThreads);
     hipLaunchKernelGGL(k_vit_approx, dim3(grid + head), dim3(kThreads), 0, s, vc, packed, g,
-                       w.comp1, grid, w.vhead);
+                       d_vt, w.comp1, grid, w.vhead);
     hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks), dim3(kScanT), 0, s, vc, packed, g,
                        w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount);
     const size_t lds3x = (size_t)(vc.emax - vc.emin + 1) * (16 + 64) * 2 * sizeof(double2);
@@ -1421,6 +1448,13 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
         hipError_t e = hipMemcpyAsync(degen_out, w.degen, nchunks, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;
     }
+    return hipGetLastError();
+}
+
+size_t vit_derived_bytes() { return sizeof(VitDerived); }
+
+hipError_t launch_vit_tables(const VitConsts& vc, VitTables* d_vt, hipStream_t s) {
+    hipLaunchKernelGGL(k_vit_tables, dim3(24), dim3(kThreads), 0, s, vc, d_vt);
     return hipGetLastError();
 }
 
