@@ -229,7 +229,7 @@ __device__ __forceinline__ int4 q_mat(const int4 q) { return make_int4(q.x, q.z,
 
 // Block 0 of every chunk starts at the chunk's first base and crosses several binades
 // (|delta| grows from ~2 to ~360 over its 256 steps), so it is always walked sequentially.
-// That walk needs nothing but the bases and the model: K1's extra "head" workgroups run it
+// That walk needs nothing but the bases and the model: extra "head" workgroups of K2's launch run it
 // (one lane per chunk, the reference step with the original constants, pipelined table
 // lookups) while the main workgroups build composites; K4 starts from its exit value.
 __device__ void vit_head(const VitConsts& vc, const uint32_t* packed, const Geo& g,
@@ -316,14 +316,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables
 
 __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uint32_t* packed,
                                                          Geo g, const VitTables* vt,
-                                                         int4* __restrict__ comp,
-                                                         unsigned main_grid,
-                                                         double2* __restrict__ vhead) {
-    if (blockIdx.x >= main_grid) {   // workgroup-uniform: head workgroups
-        vit_head(vc, packed, g, (int64_t)(blockIdx.x - main_grid) * kThreads + threadIdx.x,
-                 vhead);
-        return;
-    }
+                                                         int4* __restrict__ comp) {
     __shared__ int4 Q[16];
     // 4-step products over 5-base windows b0..b4 (exact: integers) [0, 1024), then the
     // 3-step products of steps 1..3 over b1..b4 [1024, 1280): block 0's first window (the
@@ -406,7 +399,12 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
                                                      uint8_t* __restrict__ degen,
                                                      VitPlan* __restrict__ plan,
                                                      int32_t* __restrict__ irrlist,
-                                                     int32_t* __restrict__ irrcount) {
+                                                     int32_t* __restrict__ irrcount,
+                                                     double2* __restrict__ vhead) {
+    if (blockIdx.x >= g.nchunks) {   // workgroup-uniform: the head workgroups (vit_head)
+        vit_head(vc, packed, g, (int64_t)(blockIdx.x - g.nchunks) * kScanT + threadIdx.x, vhead);
+        return;
+    }
     const int64_t c = blockIdx.x;
     const int t = threadIdx.x;
     const uint32_t* pk = chunk_ptr(packed, g, c);
@@ -727,7 +725,7 @@ __device__ __forceinline__ void st_c64(double4* p, const C64& c) {
 constexpr int kChainT = 1024;
 constexpr int kMaxStagedBar = 64;     // barriers staged in LDS per chunk
 constexpr int kStageSteps = 512;      // window steps staged in LDS per chunk (block 0
-                                      // is walked by K1's head lanes, not here)
+                                      // is walked by K2's head lanes, not here)
 __device__ __forceinline__ double2 chain_window(const uint32_t* __restrict__ pk,
                                                 const double4* sL, double4* stepL, int64_t k,
                                                 int ja, int jb, double2 v, int lane) {
@@ -788,7 +786,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     int32_t* blc = barlist + c * g.nsb;
     double2* voc = vout + c * g.nsb;
 
-    // block 0's exit value (K1's head lanes), needed by the serial chain: read now, so that its
+    // block 0's exit value (K2's head lanes), needed by the serial chain: read now, so that its
     // latency is not on the chain
     const double2 vhead0 = t == 0 ? vhead[c] : make_double2(0.0, 0.0);
     CPG_CHAIN_MARK(T0)
@@ -852,7 +850,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
                 const bool seq = xp[i].type == PLAN_SEQ;
                 kinds |= (reg ? 1u : spl ? 2u : seq ? 3u : 0u) << (2 * i);
                 const uint32_t ja = spl ? xp[i].t1 : g.jfirst(k), jb = spl ? xp[i].t2 : g.jend(k);
-                wab[i] = k == 0 ? 0u : (ja | (jb << 16));   // block 0: walked by K1's head lanes
+                wab[i] = k == 0 ? 0u : (ja | (jb << 16));   // block 0: walked by K2's head lanes
             }
     } else {
         for (int64_t k = b0; k < b1; ++k)
@@ -944,7 +942,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         sWk[t] = k;
         sWa[t] = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
         sWb[t] = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
-        if (k == 0) sWa[t] = sWb[t] = 0;   // block 0: walked by K1's head lanes
+        if (k == 0) sWa[t] = sWb[t] = 0;   // block 0: walked by K2's head lanes
         sGap[t] = ld_c64(gpc + t);
     }
     __syncthreads();
@@ -1425,11 +1423,13 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     Geo g{nchunks, chunk_len, nsb};
     const int64_t nt = nchunks * nsb;
     const unsigned grid = (unsigned)((nt + kThreads - 1) / kThreads);
-    const unsigned head = (unsigned)((nchunks + kThreads - 1) / kThreads);
-    hipLaunchKernelGGL(k_vit_approx, dim3(grid + head), dim3(kThreads), 0, s, vc, packed, g,
-                       d_vt, w.comp1, grid, w.vhead);
-    hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks), dim3(kScanT), 0, s, vc, packed, g,
-                       w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount);
+    // block 0 of every chunk is walked by extra workgroups of K2's launch (one lane per chunk):
+    // a 256-step dependent chain that would set K1's duration, hidden behind K2's scans
+    const unsigned head = (unsigned)((nchunks + kScanT - 1) / kScanT);
+    hipLaunchKernelGGL(k_vit_approx, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, d_vt,
+                       w.comp1);
+    hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks + head), dim3(kScanT), 0, s, vc, packed,
+                       g, w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount, w.vhead);
     const size_t lds3x = (size_t)(vc.emax - vc.emin + 1) * (16 + 64) * 2 * sizeof(double2);
     // K3 + K3b in one launch: the chunks' irregular blocks run as extra workgroups
     hipLaunchKernelGGL(k_vit_exact, dim3(grid + (unsigned)nchunks), dim3(kThreads), lds3x, s, vc,
