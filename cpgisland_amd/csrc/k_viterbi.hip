@@ -427,10 +427,27 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
         if (t == 0) irrcount[c] = 0;
         return;
     }
+    // a lane's (<= kPre2 for chunks up to 1 Mi) composites are loaded up front, all in flight,
+    // and kept in registers for the classification pass (no second, dependent read per block)
+    constexpr int kPre2 = 4;
+    const int cnt = (int)(b1 - b0);
+    const bool pre = cnt <= kPre2;
+    CI xs[kPre2];
     CI prod = ci_id();
-    for (int64_t k = b0; k < b1; ++k) {
-        const int4 x = cc[k];
-        prod = ci_mul(prod, CI{x.x, x.y, x.z, x.w});
+    if (pre) {
+#pragma unroll
+        for (int i = 0; i < kPre2; ++i) {
+            const int4 x = cc[cnt > 0 ? b0 + (i < cnt ? i : 0) : 0];
+            xs[i] = CI{x.x, x.y, x.z, x.w};
+        }
+#pragma unroll
+        for (int i = 0; i < kPre2; ++i)
+            if (i < cnt) prod = ci_mul(prod, xs[i]);
+    } else {
+        for (int64_t k = b0; k < b1; ++k) {
+            const int4 x = cc[k];
+            prod = ci_mul(prod, CI{x.x, x.y, x.z, x.w});
+        }
     }
     // exclusive scan of the lanes' products: shuffles inside each wave, then the wave totals
     const int lane = t & 63, wv = t >> 6;
@@ -449,16 +466,25 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
     const int f = vc.qshift;
     int64_t P = fix_of(lp, f), M = fix_of(lm, f);
     if (t > 0) ci_apply(P, M, excl);
-    for (int64_t k = b0; k < b1; ++k) {
+    auto block = [&](int64_t k, const CI& x) {
         const longlong2 en = make_longlong2(P, M);
-        const int4 x = cc[k];
-        ci_apply(P, M, CI{x.x, x.y, x.z, x.w});
+        ci_apply(P, M, x);
         bool irregular;
         pl[k] = classify(vc, g, k, en, make_longlong2(P, M), irregular);
         if (irregular) {   // only K3b reads the entry estimates (one workgroup writes a
                            // chunk's records at one CU's share of the memory system)
             ae[k] = en;
             irrlist[c * g.nsb + atomicAdd(&sIrr, 1)] = (int32_t)k;
+        }
+    };
+    if (pre) {
+#pragma unroll
+        for (int i = 0; i < kPre2; ++i)
+            if (i < cnt) block(b0 + i, xs[i]);
+    } else {
+        for (int64_t k = b0; k < b1; ++k) {
+            const int4 x = cc[k];
+            block(k, CI{x.x, x.y, x.z, x.w});
         }
     }
     __syncthreads();
@@ -1424,7 +1450,8 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     const int64_t nt = nchunks * nsb;
     const unsigned grid = (unsigned)((nt + kThreads - 1) / kThreads);
     // block 0 of every chunk is walked by extra workgroups of K2's launch (one lane per chunk):
-    // a 256-step dependent chain that would set K1's duration, hidden behind K2's scans
+    // a 256-step dependent chain (~13 us) that set K1's duration; K2 takes as long without it
+    // (as K3's extra workgroups it cost K3 0.9 us more: measured, not kept)
     const unsigned head = (unsigned)((nchunks + kScanT - 1) / kScanT);
     hipLaunchKernelGGL(k_vit_approx, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, d_vt,
                        w.comp1);
