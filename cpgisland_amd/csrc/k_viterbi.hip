@@ -1291,8 +1291,23 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
     const double2 fin = entry[c * (g.nsb + 1) + g.nsb];
     const uint32_t s_end = (fin.y > fin.x) ? 0u : 1u;   // '+' first: '-' only if strictly >
     if (t == 0 && score) score[c] = s_end ? fin.x : fin.y;
+    // chunks of 1 Mi (nsb = 4096): a lane's 16 origin maps are one 16-B load and its 16 end
+    // states one 16-B store (byte loops had issued 16 dependent loads and 16 byte stores)
+    const bool vec = per == 16 && g.nsb % 16 == 0, have = b0 < b1;
+    uint32_t ow[4] = {0, 0, 0, 0};
+    if (vec && have) {
+        const uint4 w = *reinterpret_cast<const uint4*>(og + b0);
+        ow[0] = w.x; ow[1] = w.y; ow[2] = w.z; ow[3] = w.w;
+    }
     uint32_t F = 0x2u;
-    for (int64_t k = b0; k < b1; ++k) F = map_compose(F, og[k]);
+    if (vec) {
+        if (have) {
+#pragma unroll
+            for (int i = 0; i < 16; ++i) F = map_compose(F, (ow[i >> 2] >> (8 * (i & 3))) & 0xFFu);
+        }
+    } else {
+        for (int64_t k = b0; k < b1; ++k) F = map_compose(F, og[k]);
+    }
     // suffix composition over the lanes: wave shuffles (down), then the wave totals
     const int lane = t & 63, wv = t >> 6;
     uint32_t x = F;
@@ -1309,9 +1324,21 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
     const uint32_t dn = __shfl_down(x, 1);
     const uint32_t G = lane < 63 ? map_compose(dn, after) : after;   // the lanes after t
     uint32_t e = map_apply(G, s_end);
-    for (int64_t k = b1 - 1; k >= b0; --k) {
-        endst[c * g.nsb + k] = (uint8_t)e;
-        e = map_apply(og[k], e);
+    if (vec) {
+        if (have) {
+            uint32_t ew[4] = {0, 0, 0, 0};
+#pragma unroll
+            for (int i = 15; i >= 0; --i) {
+                ew[i >> 2] |= e << (8 * (i & 3));
+                e = map_apply((ow[i >> 2] >> (8 * (i & 3))) & 0xFFu, e);
+            }
+            *reinterpret_cast<uint4*>(endst + c * g.nsb + b0) = make_uint4(ew[0], ew[1], ew[2], ew[3]);
+        }
+    } else {
+        for (int64_t k = b1 - 1; k >= b0; --k) {
+            endst[c * g.nsb + k] = (uint8_t)e;
+            e = map_apply(og[k], e);
+        }
     }
 }
 
