@@ -216,6 +216,10 @@ int cpg_sync(cpg_ctx* ctx, void* stream) {
     if (st) {
         CPG_HIP(hipMemsetAsync(ctx->d_status, 0, 4, s));
         CPG_HIP(hipStreamSynchronize(s));
+        if (st & ST_LOOKBACK_TIMEOUT)
+            return set_error(CPG_E_DEVICE,
+                             "island records: the look-back over earlier chunks' counts timed "
+                             "out; records and count are unusable (status 0x%x)", st);
         if (st == ST_CONTIG_LAYOUT)
             return set_error(CPG_E_INVALID,
                              "contig batch: a contig breaks the layout contract (offset %% 64, "
@@ -296,7 +300,7 @@ int cpg_islands_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign
     void* ws;
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &ws))) return rc;
     CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, 0, ws, ctx->ws[WS_ISL].bytes, d_out,
-                           cap, d_count, pick(ctx, stream)));
+                           cap, d_count, ctx->d_status, pick(ctx, stream)));
     return CPG_OK;
 }
 
@@ -313,7 +317,8 @@ int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_s
     void* ws;
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &ws))) return rc;
     CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, first_chunk, ws,
-                           ctx->ws[WS_ISL].bytes, d_out, cap, d_count, pick(ctx, stream)));
+                           ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status,
+                           pick(ctx, stream)));
     return CPG_OK;
 }
 

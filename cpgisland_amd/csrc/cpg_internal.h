@@ -31,6 +31,7 @@ enum : uint32_t {
     ST_VERIFY_MAG = 1u << 1,     // K3 composite outside the exact range
     ST_VERIFY_CHAIN = 1u << 2,   // K7 traceback start state mismatch
     ST_CONTIG_LAYOUT = 1u << 3,  // a contig breaks the batch layout contract (skipped)
+    ST_LOOKBACK_TIMEOUT = 1u << 4,   // a bounded look-back spin gave up (records unusable)
 };
 
 // ---- Viterbi constants (host-computed, shared by every kernel) ---------------------
@@ -132,8 +133,8 @@ hipError_t launch_vit_tables(const VitConsts& vc, VitTables* d_vt, hipStream_t s
 int64_t vit_nsb(int64_t chunk_len);
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* ws, size_t ws_bytes,
-                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s,
-                          const int64_t* base_in = nullptr);
+                          cpg_island* out, int64_t cap, int64_t* count, uint32_t* status,
+                          hipStream_t s, const int64_t* base_in = nullptr);
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
 // gtab: the model's one-step tables in device memory (est_tables); needed with PART_ACC
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,

@@ -190,7 +190,7 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
                                        sdec));
                 CPG_HIP(launch_islands(buf_packed(b), buf_out(b), nd, D, chunk0 + start / D, ws_isl,
                                        ctx->ws[WS_ISL].bytes, d_isl, island_cap, d_icnt + k + 1,
-                                       sdec, d_icnt + k));
+                                       ctx->d_status, sdec, d_icnt + k));
             } else {
                 CPG_HIP(hipMemcpyAsync(d_icnt + k + 1, d_icnt + k, 8, hipMemcpyDeviceToDevice, sdec));
             }

@@ -403,6 +403,7 @@ struct IslOut {
     const int64_t* base_in;    // append mode: records already written before this call
     int64_t first_chunk;
     uint32_t epoch;            // tags this call's look-back flags
+    uint32_t* status;          // ctx status word: ST_LOOKBACK_TIMEOUT when a spin gives up
 };
 
 __device__ __forceinline__ void put_island(const IslOut& o, const RunStat& rs, uint32_t stale_in,
@@ -421,23 +422,38 @@ __device__ __forceinline__ void put_island(const IslOut& o, const RunStat& rs, u
 
 // kept islands of the chunks before c: a look-back over their flags (this call's epoch),
 // one wave, windows of 64 chunks.  Workgroups start in chunk order, so every chunk waited
-// on is running or done; the spin is bounded all the same (2 s of wall clock).
-__device__ __forceinline__ long long kept_before(const IslWs& ws, int64_t c, uint32_t epoch) {
+// on is running or done; the spin is bounded all the same (2 s of wall clock).  A spin that
+// gives up sets ST_LOOKBACK_TIMEOUT in the status word (cpg_sync then fails the call: the
+// offsets, and so every record and the count, are unusable) and counts nothing for that
+// chunk.  CPG_ISL_SPIN_LIMIT (ticks of the 100 MHz wall clock) is a test hook.
+#ifndef CPG_ISL_SPIN_LIMIT
+#define CPG_ISL_SPIN_LIMIT 200000000ull
+#endif
+__device__ __forceinline__ long long kept_before(const IslWs& ws, int64_t c, uint32_t epoch,
+                                                 uint32_t* status) {
     const int lane = threadIdx.x & 63;
     long long sum = 0;
+    bool gave_up = false;
     const unsigned long long t0 = wall_clock64();
     for (int64_t j0 = c - 1; j0 >= 0; j0 -= 64) {
         const int64_t j = j0 - lane;
         if (j >= 0) {
             unsigned long long f;
             for (;;) {
+                // deadline first: a limit of 0 gives up deterministically (the test hook)
+                if (wall_clock64() - t0 >= (unsigned long long)(CPG_ISL_SPIN_LIMIT)) {
+                    gave_up = true;
+                    f = 0;
+                    break;
+                }
                 f = __hip_atomic_load(ws.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)(f >> 32) == epoch || wall_clock64() - t0 > 200000000ull) break;
+                if ((uint32_t)(f >> 32) == epoch) break;
                 __builtin_amdgcn_s_sleep(1);
             }
             sum += (long long)(uint32_t)f;
         }
     }
+    if (gave_up) atomicOr(status, ST_LOOKBACK_TIMEOUT);
 #pragma unroll
     for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
     return sum;
@@ -492,7 +508,7 @@ __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws
         __hip_atomic_store(ws.flags + c, ((unsigned long long)o.epoch << 32) | (uint32_t)nkt,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t < 64) {
-        const long long before = kept_before(ws, c, o.epoch);
+        const long long before = kept_before(ws, c, o.epoch, o.status);
         if (t == 0) *sbase = before;
     }
     __syncthreads();
@@ -564,8 +580,8 @@ size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len) {
 
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* wsp, size_t ws_bytes,
-                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s,
-                          const int64_t* base_in) {
+                          cpg_island* out, int64_t cap, int64_t* count, uint32_t* status,
+                          hipStream_t s, const int64_t* base_in) {
     IslWs ws = carve_isl(wsp, nchunks, chunk_len);
     if (ws.bytes > ws_bytes) return hipErrorInvalidValue;
     if (nchunks == 0)
@@ -577,7 +593,7 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
     static std::atomic<uint32_t> epoch_ctr{0};
     uint32_t epoch = ++epoch_ctr;
     if (epoch == 0) epoch = ++epoch_ctr;
-    const IslOut o{out, cap, count, base_in, first_chunk, epoch};
+    const IslOut o{out, cap, count, base_in, first_chunk, epoch, status};
     hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed,
                        chunk_len, ws, o);
     return hipGetLastError();

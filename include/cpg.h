@@ -109,7 +109,9 @@ int         cpg_abi_version(void);
  * _d entry points never allocate (required before hipGraph capture). */
 int         cpg_reserve(cpg_ctx* ctx, int64_t nbases);
 /* Wait for `stream` and return the first kernel-reported status since the last
- * cpg_sync (CPG_OK or CPG_E_VERIFY / CPG_E_UNSUPPORTED). */
+ * cpg_sync (CPG_OK, CPG_E_VERIFY, CPG_E_INVALID for a broken contig layout, or
+ * CPG_E_DEVICE when the island kernel's bounded look-back gave up: the island records
+ * and count of that call are then unusable). */
 int         cpg_sync(cpg_ctx* ctx, void* stream);
 /* A HIP stream whose kernels run only on the compute units set in cu_mask (mask_words
  * 32-bit words, bit i = compute unit i in the runtime's order): partitions the GPU between

@@ -130,6 +130,27 @@ def test_viterbi_small_chunks(gpu_ctx, torch_dev, C):
         assert sc[c] == best
 
 
+@pytest.mark.parametrize("nsb,trim", [(3856, 0), (3856, 100), (3968, 0)])
+def test_viterbi_partly_filled_tscan_lanes(gpu_ctx, torch_dev, nsb, trim):
+    """Chunk lengths whose 256-position block count nsb is in (3840, 4096] and a multiple of
+    16 take K6's 16-B path with some lanes owning no block (nsb = 3856: lanes 241-255);
+    trim > 0: one chunk with a partly filled last block."""
+    from cpgisland_amd import device as D
+    C = nsb * 256 - trim
+    nch = 1 if trim else 2
+    N = nch * C + 777
+    packed, sign = D.synth_host(4000 + nsb + trim, 0, N)
+    obs = pr.unpack(packed, N)
+    m = co.initial_model()
+    dp, _ = _dev_genome(packed, sign, torch_dev)
+    sg, sc = _viterbi(gpu_ctx, m, dp, N, C)
+    states, _, score = co.decode_chunks(m, obs, C)
+    assert len(states) == nch * C
+    assert np.array_equal(sg[:nch * C], (states < 4).astype(np.uint8))
+    assert not sg[nch * C:].any()
+    assert np.array_equal(sc, score)
+
+
 def test_viterbi_adversarial_inputs(gpu_ctx, torch_dev):
     m = co.initial_model()
     n = DECODE
@@ -337,6 +358,54 @@ def test_islands_long_overflow_island(gpu_ctx, torch_dev):
                          pr.pack_bits((st < 4).astype(np.uint8)), torch_dev)
     out, cnt = D.islands(gpu_ctx, dp, ds, C, C)
     assert np.array_equal(D.islands_to_numpy(out, cnt), co.islands(st, 0))
+
+
+def test_islands_lookback_timeout_is_an_error(gpu_ctx):
+    """The island kernel's look-back over earlier chunks' kept counts is a bounded spin.
+    libcpg_isl_timeout.so is built with that bound forced to 0 (CPG_ISL_SPIN_LIMIT=0), so
+    every chunk after the first gives up: the call must fail with CPG_E_DEVICE (status bit
+    ST_LOOKBACK_TIMEOUT via cpg_sync) instead of returning records at wrong offsets."""
+    import ctypes as C
+    import os
+    from cpgisland_amd import _lib
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libcpg_isl_timeout.so")
+    assert os.path.exists(path), "build it: make -C cpgisland_amd/csrc"
+    lib = C.CDLL(path)
+    lib.cpg_open.argtypes = [C.c_int, C.c_void_p]
+    lib.cpg_close.argtypes = [C.c_void_p]
+    lib.cpg_last_error.restype = C.c_char_p
+    lib.cpg_islands.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                C.c_void_p, C.c_int64, C.c_void_p]
+    rng = np.random.default_rng(7)
+    CL, nch = 4096, 8
+    states = np.concatenate([np.resize(_rand_states(rng), CL) for _ in range(nch)])
+    packed = np.ascontiguousarray(pr.pack((states % 4).astype(np.uint8)).astype(np.uint32))
+    sign = np.ascontiguousarray(pr.pack_bits((states < 4).astype(np.uint8)).astype(np.uint32))
+    out = np.zeros(4096, co.ISLAND_DTYPE)
+    cnt = C.c_int64(0)
+    ctx = C.c_void_p()
+    assert lib.cpg_open(0, C.byref(ctx)) == 0
+    try:
+        rc = lib.cpg_islands(ctx, packed.ctypes.data, sign.ctypes.data, nch * CL, CL,
+                             out.ctypes.data, len(out), C.byref(cnt))
+        assert rc == _lib.CPG_E_DEVICE, rc
+        assert b"look-back" in lib.cpg_last_error()
+        # the status word was consumed: the same context works again for one chunk
+        rc1 = lib.cpg_islands(ctx, packed.ctypes.data, sign.ctypes.data, CL, CL,
+                              out.ctypes.data, len(out), C.byref(cnt))
+        assert rc1 == 0
+        exp = co.islands(states[:CL], 0)
+        assert np.array_equal(out[:cnt.value], exp)
+    finally:
+        lib.cpg_close(ctx)
+    # the product library on the same input: no timeout, oracle records
+    from cpgisland_amd import device as D
+    import torch
+    dev = torch.device("cuda:0")
+    dp, ds = _dev_genome(packed, sign, dev)
+    o2, c2 = D.islands(gpu_ctx, dp, ds, nch * CL, CL)
+    exp = np.concatenate([co.islands(states[c * CL:(c + 1) * CL], c) for c in range(nch)])
+    assert np.array_equal(D.islands_to_numpy(o2, c2), exp)
 
 
 def test_islands_capacity(gpu_ctx, torch_dev, golden):
