@@ -174,6 +174,10 @@ def main():
                     help="record HIP events around every phase (default: E-step and decode)")
     ap.add_argument("--decode-event-every", type=int, default=4,
                     help="record the decode phase's events on every k-th timed step")
+    ap.add_argument("--estep-event-every", type=int, default=4,
+                    help="record the E-step phase's events on every k-th timed step (an event "
+                         "record is a release at its point in the stream: ~6 us of train-stream "
+                         "gap each)")
     ap.add_argument("--no-phase-events", action="store_true",
                     help="(diagnostic) record no per-phase HIP events inside the timed steps")
     ap.add_argument("--decode-split", type=int, default=1,
@@ -304,7 +308,11 @@ def main():
         def mark(name, i):
             if it is None or args.no_phase_events:
                 return
-            if full_ev or name == "estep":
+            if full_ev:
+                key = name
+            elif name == "estep":
+                if it % args.estep_event_every:
+                    return
                 key = name
             elif (name, i) in (("viterbi", 0), ("islands", 1)) and it % args.decode_event_every == 0:
                 key, i = "decode", (0 if name == "viterbi" else 1)
@@ -440,7 +448,7 @@ def main():
                           "step_overlap": not (args.no_overlap or args.serial),
                           "pipeline_lanes": nlanes,
                           "phase_events": ("all" if full_ev else
-                                           f"estep every step, decode every {args.decode_event_every}"),
+                                           f"estep every {args.estep_event_every}, decode every {args.decode_event_every}"),
                           "train_cus": len(tr_cus) if tr_cus else ncu,
                           "bases_per_gpu": N, "train_chunk": TRAIN, "decode_chunk": DECODE,
                           "decode_chunks_per_gpu": ndec, "parallelism": f"dp{world}",

@@ -62,6 +62,31 @@ struct __attribute__((aligned(8))) VitPlan {
     uint16_t t2;     // offset where the post composite starts
 };
 
+// ---- last-workgroup finalize (device) ----------------------------------------------
+// The accumulating kernels (counts, E-step) fold their one-workgroup finalize into the main
+// launch: every workgroup's accumulator atomics are device-scope RMWs (performed at the
+// device coherence point, past the XCD-private L2s) and have completed once the workgroup has
+// drained its memory counters; then thread 0 counts the workgroup in, and the workgroup that
+// counts last reads the accumulators with device-scope loads.  No L2 writeback fence is
+// needed (the only data exchanged is atomics): a release per workgroup would write back the
+// XCD's L2, including what concurrent kernels on the other stream have written.
+#ifdef __HIPCC__
+__device__ __forceinline__ bool last_workgroup(unsigned int* done, int* s_flag) {
+    __builtin_amdgcn_s_waitcnt(0);   // this wave's atomics have completed
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const unsigned prev =
+            __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        *s_flag = prev == gridDim.x - 1;
+    }
+    __syncthreads();
+    return *s_flag != 0;
+}
+__device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+#endif
+
 // ---- context -----------------------------------------------------------------------
 struct Buf {
     void* p = nullptr;

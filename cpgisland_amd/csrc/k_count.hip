@@ -10,9 +10,10 @@
 //
 // Per-workgroup partial counts (and the init states of the chunks starting in the
 // workgroup) are added to 72 global 64-bit accumulators (integer atomics: exact and
-// order-independent, one per counter per workgroup); a one-workgroup finalize derives the
+// order-independent, one per counter per workgroup); the last workgroup to finish derives the
 // emission/dinucleotide/mono counts from the transition + init counts (exact integer
-// identities) and re-zeroes the accumulators.  Two launches per call.
+// identities) and re-zeroes the accumulators.  One launch per call (a separate one-workgroup
+// finalize launch for the streamed genome, which accumulates every window first).
 
 #include "cpg_internal.h"
 
@@ -57,11 +58,15 @@ __device__ __forceinline__ uint32_t spread16(uint32_t x) {
 }
 
 __device__ void final_counts(const uint64_t* raw, int t, int64_t* __restrict__ out);
+template <bool kAgent>
+__device__ void finalize(unsigned long long* gacc, uint64_t* raw, int64_t* out);
 
+// done != nullptr: the last workgroup to finish also finalizes (one launch per call)
 __global__ __launch_bounds__(kCountThreads) void k_count_main(
     const uint4* __restrict__ packed4, const uint2* __restrict__ sign2,
     const uint32_t* __restrict__ packed, const uint32_t* __restrict__ sign, int64_t nblk,
-    int64_t blk_per_chunk, unsigned long long* __restrict__ gacc) {
+    int64_t blk_per_chunk, unsigned long long* __restrict__ gacc, unsigned int* done,
+    int64_t* __restrict__ out) {
     uint32_t tot[16], pp[16], pm[16], mp[16];
 #pragma unroll
     for (int d = 0; d < 16; ++d) tot[d] = pp[d] = pm[d] = mp[d] = 0u;
@@ -180,21 +185,35 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
             atomicAdd(gacc + (blockIdx.x % kCntRep) * kRaw + threadIdx.x,
                            (unsigned long long)acc);
     }
+    __shared__ int s_last;
+    __shared__ uint64_t raw[kRaw];
+    if (done && last_workgroup(done, &s_last)) {
+        finalize<true>(gacc, raw, out);
+        if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+// the cpg_counts_i64 assembly from the 72 accumulators (replicas summed), which it re-zeroes;
+// kAgent: the accumulators were written by workgroups of the same launch
+template <bool kAgent>
+__device__ void finalize(unsigned long long* gacc, uint64_t* raw, int64_t* out) {
+    const int t = threadIdx.x;
+    if (t < kRaw) {
+        uint64_t v = 0;
+        for (int r = 0; r < kCntRep; ++r)
+            v += kAgent ? load_agent(gacc + r * kRaw + t) : gacc[r * kRaw + t];
+        raw[t] = v;
+    }
+    __syncthreads();
+    for (int i = t; i < kRaw * kCntRep; i += blockDim.x) gacc[i] = 0ull;
+    for (int i = t; i < 124; i += blockDim.x) final_counts(raw, i, out);
 }
 
 // One workgroup: the cpg_counts_i64 assembly from the 72 accumulators, which it re-zeroes.
 __global__ __launch_bounds__(128) void k_count_final(unsigned long long* __restrict__ gacc,
                                                      int64_t* __restrict__ out) {
     __shared__ uint64_t raw[kRaw];
-    const int t = threadIdx.x;
-    if (t < kRaw) {
-        uint64_t v = 0;
-        for (int r = 0; r < kCntRep; ++r) v += gacc[r * kRaw + t];
-        raw[t] = v;
-    }
-    __syncthreads();
-    for (int i = t; i < kRaw * kCntRep; i += blockDim.x) gacc[i] = 0ull;
-    if (t < 124) final_counts(raw, t, out);
+    finalize<false>(gacc, raw, out);
 }
 
 // cpg_counts_i64 from the 72 raw sums (tot | pp | pm | mp | init); thread t < 124
@@ -244,15 +263,18 @@ hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nc
         int grid = CNT_GRID;
         if ((int64_t)grid * kCountThreads > nblk)
             grid = (int)((nblk + kCountThreads - 1) / kCountThreads);
+        // the whole call in one launch: its last workgroup finalizes
+        unsigned int* done = parts == PART_ALL ? (unsigned int*)(ws + kRaw * kCntRep) : nullptr;
         hipLaunchKernelGGL(k_count_main, dim3(grid), dim3(kCountThreads), 0, s,
                            (const uint4*)packed, (const uint2*)sign, packed, sign, nblk,
-                           chunk_len / 64, (unsigned long long*)ws);
+                           chunk_len / 64, (unsigned long long*)ws, done, out);
+        if (done) return hipGetLastError();
     }
     if (parts & PART_FINAL)
         hipLaunchKernelGGL(k_count_final, dim3(1), dim3(128), 0, s, (unsigned long long*)ws, out);
     return hipGetLastError();
 }
 
-size_t count_ws_bytes(int64_t) { return (size_t)kRaw * 8 * kCntRep; }
+size_t count_ws_bytes(int64_t) { return (size_t)kRaw * 8 * kCntRep + 64; }   // + done counter
 
 }  // namespace cpg

@@ -9,18 +9,19 @@
 //   1. each lane forms the product of its 64 matrices (power-of-two exponent tracking);
 //   2. workgroup prefix / suffix scans give the forward vector entering and the backward
 //      vector leaving every lane's 64 positions;
-//   3. each lane walks its positions in 16-position mini-blocks: forward alphas kept in
-//      registers, backward betas from 3 checkpoints, posterior pair marginals xi_p(i,j)
-//      = alpha_{p-1}(i) M_p(i,j) beta_p(j) / Z_p accumulated into per-wave LDS bins in
-//      unsigned fixed point (2^-47, round to nearest) with integer LDS atomics: exact,
-//      order-independent sums (measured: fp64 LDS atomics were 2x the integer ones).
+//   3. each lane walks its positions in 16-position mini-blocks, last to first: forward
+//      alphas recomputed into registers from 3 checkpoints, then the backward chain with the
+//      posterior pair marginals xi_p(i,j) = alpha_{p-1}(i) M_p(i,j) beta_p(j) / Z, beta
+//      pre-scaled by 2^47 / Z so that each xi is one fma onto the integer grid (unsigned fixed
+//      point 2^-47, round to nearest), accumulated into LDS bins with integer LDS atomics:
+//      exact, order-independent sums (measured: fp64 LDS atomics were 2x the integer ones).
 // Posteriors are normalised per position, so the scaling scheme (exact powers of two here,
 // reciprocal of the sum in the reference) changes results only at rounding level: parity
 // with the oracle is by tolerance (tests: 1e-9 relative).  Emission counts follow exactly
 // from sum_i xi(i,j) = gamma(j): emit[j] = init[j] + column sum j of trans.
 // Per-chunk results are added to 128-bit fixed-point accumulators (64-bit integer atomics
-// with carry into a high word: exact, order-independent, so deterministic); a
-// one-workgroup finalize converts them to the cpg_counts_f64 stripes.
+// with carry into a high word: exact, order-independent, so deterministic); the last
+// workgroup to finish converts them to the cpg_counts_f64 stripes (one launch per call).
 
 #include <algorithm>
 #include <cmath>
@@ -50,32 +51,16 @@ constexpr int kSlab = 73;               // trans[64] (by dinucleotide x 4) | ini
 #define EST_ACC_REP 16
 #endif
 constexpr int kAccRep = EST_ACC_REP;
-// xi bins of one 16-lane replica: [k = from,to pair][d] (64 x u64) padded to 80 so that the
-// two replicas an LDS pass serves sit in opposite bank halves (80 * 8 B = 640 B = 160 banks)
-#ifndef EST_REP
-#define EST_REP 80
-#endif
-#ifndef EST_KD
-#define EST_KD 1
-#endif
-constexpr int kRep = EST_REP;
-#ifndef EST_NREP
-#define EST_NREP 4
-#endif
-constexpr int kNRep = EST_NREP;   // bin replicas per wave (64 / kNRep lanes share one)
-// EST_BINS 1: one bin set of 64 rows (d, k) x 16 columns (u64), lane column = lane % 16.
-// An LDS 64-bit access serves 16 lanes per cycle with bank = (address / 4) mod 32: the 16
-// lanes of a pass always hit 16 different columns = 32 different banks, whatever their
-// classes — no bank conflicts and no same-address collisions inside a pass (the replicated
-// per-wave sets of EST_BINS 0 collide whenever two lanes of a pass share a class).
-#ifndef EST_BINS
-#define EST_BINS 1
-#endif
+// xi bins: ONE set of 64 rows (k = pair, d = class: row k * 16 + d) x 16 columns (u64), lane
+// column = lane % 16.  An LDS 64-bit access serves 16 lanes per cycle with bank = (address /
+// 4) mod 32: the 16 lanes of a pass always hit 16 different columns = 32 different banks,
+// whatever their classes — no bank conflicts and no same-address collisions inside a pass
+// (per-wave replicated sets, measured earlier, collide whenever two lanes of a pass share a
+// class).
 // LDS: TA/TB (512 B) | union { 4-step tables, scan buffer, bins } | per-wave partials
 constexpr size_t kUnionOff = 32 * 16;
-constexpr size_t kUnionBytes =
-    (size_t)16 * kNRep * kRep * 8 > 2048 * 16 ? (size_t)16 * kNRep * kRep * 8 : 2048 * 16;
-__device__ __forceinline__ int bin_of(int d, int k) { return EST_KD ? k * 16 + d : d * 4 + k; }
+constexpr size_t kUnionBytes = 2048 * 16;
+__device__ __forceinline__ int bin_of(int d, int k) { return k * 16 + d; }
 
 struct Mat {
     double a, b, c, d;   // [[a b] [c d]]
@@ -185,6 +170,23 @@ __device__ __forceinline__ unsigned long long to_fixed_scaled(double y) {   // y
     return (unsigned long long)__double_as_longlong(y + kMagic) -
            (unsigned long long)__double_as_longlong(kMagic);
 }
+// K + round(a * b) for a * b in [0, 2^51), K = the bit pattern of 1.5*2^52: one fma onto the
+// integer grid, its bits taken as they are.  The xi bins sum these raw patterns; K is removed
+// per bin once per chunk (class_count below), not per value.
+constexpr unsigned long long kMagicBits = 0x4338000000000000ull;
+__device__ __forceinline__ unsigned long long raw_fma(double a, double b) {
+    return (unsigned long long)__double_as_longlong(fma(a, b, kMagic));
+}
+// Every position of class d adds one raw value to each of its 4 bins (k = pair), so all 4 hold
+// n_d * K + sum_k y (mod 2^64), and the 4 pairs' y sum to 2^47 per position up to rounding
+// (|e| <= 3 per position): S = sum of the 4 = n_d * (4K + 2^47) + e (mod 2^64), where
+// 4K + 2^47 = 0x0CE08 << 44 (mod 2^64) and |e| < 2^43.  Bits 44..63 of S (rounded) give
+// n_d * 0x0CE08 mod 2^20 = 8 * (n_d * 0x19C1 mod 2^17), and 0x19C1 is odd: n_d (< 2^17) is
+// that times its inverse mod 2^17 (0xF641).
+__device__ __forceinline__ unsigned long long class_count(unsigned long long S) {
+    const unsigned long long q = ((S + (1ull << 43)) >> 44) & 0xFFFFFull;
+    return ((q >> 3) * 0xF641ull) & 0x1FFFFull;
+}
 constexpr int kLogFix = 24;   // log-likelihood fixed point: 2^-24 (|chunk loglik| < 2^30)
 
 // 128-bit two's-complement accumulation with 64-bit atomics: the adder that wraps the low
@@ -251,6 +253,10 @@ __device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int
     return c;
 }
 
+template <bool kAgent>
+__device__ void finalize(unsigned long long* acc, double* vsum, double* out);
+__device__ void final_estep(const double* v, int t, double* __restrict__ out);
+
 #ifdef CPG_DEBUG_ESTEP
 #define CPG_EST_MARK(n) const unsigned long long n = wall_clock64();
 #else
@@ -262,11 +268,9 @@ __device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int
 #define CPG_EST_WPE 4
 #endif
 __global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(CPG_EST_WPE)))
-void k_estep_chunk(const cpg_model model,
-                                                     const uint32_t* __restrict__ packed,
-                                                     int64_t C,
-                                                     unsigned long long* __restrict__ acc,
-                                                     const double2* __restrict__ gtab) {
+void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
+                   unsigned long long* __restrict__ acc, const double2* __restrict__ gtab,
+                   unsigned int* done, double* __restrict__ out) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves
@@ -277,7 +281,7 @@ void k_estep_chunk(const cpg_model model,
     // buffer (phase 2), the xi bins (phase 3) — each phase ends with a barrier
     double2* TA4 = TB + 16;                                   // 4-step products, row 0
     double2* TB4 = TA4 + 1024;                                //                  row 1
-    auto* bins = reinterpret_cast<unsigned long long*>(TA4);  // [wave][kNRep][kRep]
+    auto* bins = reinterpret_cast<unsigned long long*>(TA4);  // [64 rows][16 columns]
     auto* part = reinterpret_cast<unsigned long long*>(
         smem + kUnionOff + kUnionBytes);
     double4* fck4 = reinterpret_cast<double4*>(part + 16 * 64);   // [NMB-1][nl] products
@@ -440,42 +444,18 @@ void k_estep_chunk(const cpg_model model,
     // 3a. bins (aliasing the scan buffer, read above) zeroed; alpha entering mini-block m
     //     = alpha entering the lane times phase 1's product of the first m mini-blocks
     //     (any per-position scale cancels in the normalised xi)
-#if EST_BINS
     for (int i = t; i < 64 * 16; i += nl) bins[i] = 0ull;
-#else
-    for (int i = t; i < nw * kNRep * kRep; i += nl) bins[i] = 0ull;
-#endif
     __syncthreads();
     CPG_EST_MARK(T5)
     // 3b. mini-blocks, last to first: forward alphas in registers from the checkpoint, then
     //     backward with xi accumulation; beta flows on from one mini-block to the previous
-#if EST_BINS
     unsigned long long* wb = bins + (lane & 15);
     constexpr int kBS = 16;   // row stride
-#else
-    unsigned long long* wb = bins + ((t >> 6) * kNRep + lane / (64 / kNRep)) * kRep;
-    constexpr int kBS = 1;
-#endif
     double g0P = 0.0, g0M = 0.0;
     double yP = bP, yM = bM;   // beta at the last position of the mini-block
-#ifndef EST_ABL
-#define EST_ABL 0
-#endif
-#ifndef EST_GTAB
-// 1: the backward pass reads its table rows from a global copy (L1-resident): those loads are
-// waited on with vmcnt, not lgkmcnt, so they do not wait for the preceding LDS atomics
-// (LDS operations retire in order); measured -5 %.  2: the forward recompute too (+20 %:
-// its chain then waits on the longer global latency).
-#define EST_GTAB 1
-#endif
-#ifndef EST_PF
-#define EST_PF 0   // prefetch the backward pass's table rows one position ahead
-#endif
-    unsigned long long sink = 0;   // ablations only
-#ifndef EST_MB_UNROLL
-#define EST_MB_UNROLL 1
-#endif
-#pragma unroll EST_MB_UNROLL
+    // (measured and dropped: mini-block m's backward pass interleaved with mini-block m-1's
+    // forward pass, two dependency chains per wave — 16 alpha pairs live either way, but the
+    // two chains' temporaries spill: 0.18 vs 0.127 ms)
     for (int m = NMB - 1; m >= 0; --m) {
         // the mini-block's codes from its packed word (L1/L2, two dwords): neither 8 live
         // VGPRs of codes nor a scratch copy of them
@@ -490,7 +470,7 @@ void k_estep_chunk(const cpg_model model,
             bfM = f.y;
         }
         double alP[kMB], alM[kMB];
-        int kf[kMB / 4];   // alpha's power-of-two shifts after positions 3, 7, 11
+        int kf[kMB / 4];   // alpha's power-of-two shifts at positions 3, 7, 11, 15
         double xP = bfP, xM = bfM;
 #pragma unroll
         for (int i = 0; i < kMB; ++i) {
@@ -500,11 +480,7 @@ void k_estep_chunk(const cpg_model model,
                 continue;
             }
             const uint32_t d = code_at(cm, i);
-#if EST_GTAB >= 2
-            const double2 ma = gtab[d], mb = gtab[16 + d];
-#else
             const double2 ma = TA[d], mb = TB[d];
-#endif
             const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
             xP = nP;
             xM = nM;
@@ -512,131 +488,101 @@ void k_estep_chunk(const cpg_model model,
             alP[i] = xP;
             alM[i] = xM;
         }
-        // Z_p = alpha_{p-1}^T M_p beta_p is the same at every position up to the exact
-        // power-of-two rescalings of alpha and beta, so one reciprocal per mini-block (at its
-        // last position) normalises every xi: rz_p = rz_15 * 2^(eb - ef), eb = beta's shifts
-        // since position 15, ef = alpha's shifts between positions p-1 and 14
-        double rz0 = 0.0, rz = 0.0;
-        int eb = 0, ef = 0;
-        // table rows of the next (lower) position are read one position ahead, before this
-        // position's LDS atomics: LDS operations retire in order, so a read issued after the
-        // atomics would make every position wait for the previous position's atomics
-#if EST_PF == 1
-        double2 pma = TA[code_at(cm, kMB - 1)], pmb = TB[code_at(cm, kMB - 1)];
-#elif EST_PF == 2
-        double2 pma = gtab[code_at(cm, kMB - 1)], pmb = gtab[16 + code_at(cm, kMB - 1)];
+        // beta pre-scaled by 2^47 / Z: with a_i = the stored (renormalised) alpha at i and
+        // s_i its shift (a_{i-1} M_i = 2^{s_i} a_i), keep  a_{i-1} . (M_i y_i) = 2^47  at
+        // every position, so xi_i(a,b) * 2^47 = a_{i-1}(a) * (M_i(a,b) y_i(b)) — one fma per
+        // pair, straight onto the fixed-point grid (fma(., ., 1.5*2^52)), no per-position
+        // normaliser.  Start: y_15 = beta_15 * 2^{47-s_15} / (a_15 . beta_15); crossing an
+        // alpha renormalisation point going backward (i-1 = 11, 7, 3) scales y by 2^{-s}.
+        // y only shrinks through M (entries <= 1) and grows by the alpha shifts of one
+        // mini-block; it is renormalised once per mini-block.
+        vnorm(yP, yM);
+        {
+            const double r = ldexp(rcp_nr(alP[kMB - 1] * yP + alM[kMB - 1] * yM), 47 - kf[3]);
+            yP *= r;
+            yM *= r;
+        }
+#ifndef EST_PFD
+#define EST_PFD 1   // backward table rows loaded this many positions ahead (2, 3: no faster)
 #endif
+        // the backward pass's table rows come from a global copy (L1-resident): waited on
+        // with vmcnt, not behind the preceding LDS atomics (LDS operations retire in order;
+        // an LDS copy read ahead of the atomics spills)
+        double2 qa[EST_PFD + 1], qb[EST_PFD + 1];
+        auto trow = [&](int i, double2& a, double2& b) {
+            const uint32_t d = code_at(cm, i);
+            a = gtab[d];
+            b = gtab[16 + d];
+        };
+#pragma unroll
+        for (int j = 0; j < EST_PFD; ++j) trow(kMB - 1 - j, qa[j], qb[j]);
 #pragma unroll
         for (int i = kMB - 1; i >= 0; --i) {
-#if EST_PF
-            const double2 cma = pma, cmb = pmb;
-            if (i > 0) {
-#if EST_PF == 2
-                pma = gtab[code_at(cm, i - 1)];
-                pmb = gtab[16 + code_at(cm, i - 1)];
-#else
-                pma = TA[code_at(cm, i - 1)];
-                pmb = TB[code_at(cm, i - 1)];
-#endif
-            }
-#else
-#if EST_GTAB   // the same rows from a global copy: waited on with vmcnt, not behind the atomics
-            const double2 cma = gtab[code_at(cm, i)], cmb = gtab[16 + code_at(cm, i)];
-#else
-            const double2 cma = TA[code_at(cm, i)], cmb = TB[code_at(cm, i)];
-#endif
-#endif
-            if (t == 0 && m == 0 && i == 0) {   // gamma_0 -> init counts
-                const double gp = alP[0] * yP, gm = alM[0] * yM, z = gp + gm;
-                g0P = gp / z;
-                g0M = gm / z;
+            // table rows issued EST_PFD positions ahead; the scheduling barrier keeps the
+            // compiler from sinking them to their use, which had put one full L1/L2 round trip
+            // (two, serialised) on every position's chain
+            if (i - EST_PFD >= 0) trow(i - EST_PFD, qa[(kMB - 1 - i + EST_PFD) % (EST_PFD + 1)],
+                                       qb[(kMB - 1 - i + EST_PFD) % (EST_PFD + 1)]);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t d = code_at(cm, i);
+            const double2 ma = qa[(kMB - 1 - i) % (EST_PFD + 1)], mb = qb[(kMB - 1 - i) % (EST_PFD + 1)];
+            if (t == 0 && m == 0 && i == 0) {   // gamma_0 = a_0 * y_0 / 2^47 -> init counts
+                g0P = alP[0] * yP;
+                g0M = alM[0] * yM;
                 continue;
             }
             const double uP = i > 0 ? alP[i - 1] : bfP;
             const double uM = i > 0 ? alM[i - 1] : bfM;
-            const uint32_t d = code_at(cm, i);
-#if EST_ABL == 3   // development ablation: no table reads in the backward pass
-            const double2 ma = make_double2(0.5 + d * 1e-3, 0.25), mb = make_double2(0.125, 0.5);
-            (void)cma;
-            (void)cmb;
-#else
-            const double2 ma = cma, mb = cmb;
-#endif
-            // M beta products, shared by the pair marginals and the beta update
+            // M y products, shared by the pair marginals and the beta update
             const double t00 = ma.x * yP, t01 = ma.y * yM, t10 = mb.x * yP, t11 = mb.y * yM;
-            const double x00 = uP * t00, x01 = uP * t01, x10 = uM * t10, x11 = uM * t11;
-            if (i == kMB - 1) {
-                rz0 = rcp_nr((x00 + x01) + (x10 + x11)) * kFix;
-                rz = rz0;
-            } else if ((i & 3) == 3) {
-                ef += kf[i >> 2];
-                rz = ldexp(rz0, eb - ef);
-            }
-#if EST_ABL == 1   // development ablation: no LDS atomics (wrong results, timing only)
-            sink += to_fixed_scaled(x00 * rz) ^ to_fixed_scaled(x01 * rz) ^
-                    to_fixed_scaled(x10 * rz) ^ to_fixed_scaled(x11 * rz) ^ d;
-#elif EST_ABL == 2   // development ablation: collision-free lane-private bins
-            {
-                unsigned long long* pb = bins + ((t & 1023) % (nw * kNRep * kRep / 4)) * 4;
-                atomicAdd(pb + 0, to_fixed_scaled(x00 * rz));
-                atomicAdd(pb + 1, to_fixed_scaled(x01 * rz));
-                atomicAdd(pb + 2, to_fixed_scaled(x10 * rz));
-                atomicAdd(pb + 3, to_fixed_scaled(x11 * rz) + d);
-            }
-#else
-            // to_fixed_scaled(x * rz) contracts to one fma(x, rz, 1.5*2^52)
-            atomicAdd(wb + bin_of(d, 0) * kBS, to_fixed_scaled(x00 * rz));
-            atomicAdd(wb + bin_of(d, 1) * kBS, to_fixed_scaled(x01 * rz));
-            atomicAdd(wb + bin_of(d, 2) * kBS, to_fixed_scaled(x10 * rz));
-            atomicAdd(wb + bin_of(d, 3) * kBS, to_fixed_scaled(x11 * rz));
-#endif
+            atomicAdd(wb + bin_of(d, 0) * kBS, raw_fma(uP, t00));
+            atomicAdd(wb + bin_of(d, 1) * kBS, raw_fma(uP, t01));
+            atomicAdd(wb + bin_of(d, 2) * kBS, raw_fma(uM, t10));
+            atomicAdd(wb + bin_of(d, 3) * kBS, raw_fma(uM, t11));
             yP = t00 + t01;
             yM = t10 + t11;
-            if ((i & 3) == 0) eb += vnorm(yP, yM);
+            if (i == 4 || i == 8 || i == 12) {
+                yP = ldexp(yP, -kf[(i - 1) >> 2]);
+                yM = ldexp(yM, -kf[(i - 1) >> 2]);
+            }
         }
     }
     __syncthreads();
     CPG_EST_MARK(T6)
-    // chunk totals of the nw * kNRep replicas: wave q sums replicas q, q + nw, ... of every
-    // bin (integer sums: exact in any order), then 64 lanes add the nw partials
-#if EST_BINS
-    if (t < 64) {   // row t = d * 4 + k: the sum of its 16 columns
+    // chunk totals: row t = d * 4 + k, the sum of its 16 columns (integer: exact in any order)
+    if (t < 64) {
         const unsigned long long* row = bins + bin_of(t >> 2, t & 3) * 16;
         unsigned long long s = 0;
 #pragma unroll
         for (int col = 0; col < 16; ++col) s += row[(col + t) & 15];   // rotated: no conflicts
         part[t] = s;
     }
-#else
-    {
-        const int q = t >> 6, b = bin_of(lane >> 2, lane & 3);   // lane = slab row d*4+k
-        unsigned long long s = 0;
-        for (int r = q; r < nw * kNRep; r += nw) s += bins[r * kRep + b];
-        part[q * 64 + lane] = s;
-    }
-#endif
     __syncthreads();
     CPG_EST_MARK(T7)
     unsigned long long* racc = acc + 2 * kSlab * (c % kAccRep);
     // chunk results -> the global 128-bit accumulators: xi bins and the init posteriors in
     // 2^-47 units, the log-likelihood in signed 2^-24 units
-    if (t < 64) {   // row t = d * 4 + k
-        unsigned long long s = 0;
-#if EST_BINS
-        s = part[t];
-#else
-        for (int q = 0; q < nw; ++q) s += part[q * 64 + t];
-#endif
+    if (t < 64) {   // row t = d * 4 + k (wave 0)
+        unsigned long long s = part[t];
+        // the class's 4 raw sums (lanes 4d .. 4d+3) -> its position count -> K removed
+        unsigned long long S = s;
+        S += __shfl_xor(S, 1);
+        S += __shfl_xor(S, 2);
+        s -= class_count(S) * kMagicBits;
         acc128_add(racc + 2 * t, s, false);
     }
-    if (EST_ABL && sink == 0x123456789ull) acc[0] = sink;   // keep the ablated work live
     if (t == 0) {
-        acc128_add(racc + 2 * (64 + o0), to_fixed_scaled(g0P * kFix), false);
-        acc128_add(racc + 2 * (64 + o0 + 4), to_fixed_scaled(g0M * kFix), false);
+        acc128_add(racc + 2 * (64 + o0), to_fixed_scaled(g0P), false);   // already 2^47-scaled
+        acc128_add(racc + 2 * (64 + o0 + 4), to_fixed_scaled(g0M), false);
     }
     if (t == nl - 1) {
         const long long L = llrint(ldexp(loglik, kLogFix));
         acc128_add(racc + 2 * 72, (unsigned long long)L, L < 0);
+    }
+    // done != nullptr: the last workgroup to finish converts the sums (one launch per call)
+    if (done && last_workgroup(done, reinterpret_cast<int*>(part))) {
+        finalize<true>(acc, reinterpret_cast<double*>(part + 2), out);
+        if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 #ifdef CPG_DEBUG_ESTEP
     if (t == 0 && (c == 0 || c == 300 || c == (int64_t)gridDim.x - 1))
@@ -647,18 +593,18 @@ void k_estep_chunk(const cpg_model model,
 }
 
 
-__device__ void final_estep(const double* v, int t, double* __restrict__ out);
-
-// One workgroup: the 73 accumulators -> doubles (re-zeroed for the next call), then the
-// cpg_counts_f64 assembly.
-__global__ __launch_bounds__(256) void k_estep_final(unsigned long long* __restrict__ acc,
-                                                     double* __restrict__ out) {
-    __shared__ double vsum[kSlab];
+// The 73 accumulators (replicas summed in 128-bit integer arithmetic) -> doubles, re-zeroed
+// for the next call, then the cpg_counts_f64 assembly.  kAgent: written by workgroups of the
+// same launch (device-scope loads).
+template <bool kAgent>
+__device__ void finalize(unsigned long long* acc, double* vsum, double* out) {
     const int t = threadIdx.x;
-    if (t < kSlab) {
+    for (int i = t; i < kSlab; i += blockDim.x) {
         unsigned long long lo = 0ull, hi = 0ull;   // 128-bit sum of the replicas
         for (int r = 0; r < kAccRep; ++r) {
-            const unsigned long long l = acc[2 * (r * kSlab + t)], h = acc[2 * (r * kSlab + t) + 1];
+            const unsigned long long* a = acc + 2 * (r * kSlab + i);
+            const unsigned long long l = kAgent ? load_agent(a) : a[0];
+            const unsigned long long h = kAgent ? load_agent(a + 1) : a[1];
             const unsigned long long nl = lo + l;
             hi += h + (nl < lo ? 1ull : 0ull);
             lo = nl;
@@ -669,11 +615,19 @@ __global__ __launch_bounds__(256) void k_estep_final(unsigned long long* __restr
             hi = ~hi + (lo == 0ull ? 1ull : 0ull);
         }
         const double mag = (double)hi * 18446744073709551616.0 + (double)lo;
-        vsum[t] = t < 72 ? mag * (1.0 / kFix) : ldexp(neg ? -mag : mag, -kLogFix);
+        vsum[i] = i < 72 ? mag * (1.0 / kFix) : ldexp(neg ? -mag : mag, -kLogFix);
     }
     __syncthreads();
     for (int i = t; i < 2 * kSlab * kAccRep; i += blockDim.x) acc[i] = 0ull;
-    if (t < 105) final_estep(vsum, t, out);
+    for (int i = t; i < 105; i += blockDim.x) final_estep(vsum, i, out);
+}
+
+// One workgroup: finalize of accumulators filled by earlier launches (streamed genome,
+// contig batches).
+__global__ __launch_bounds__(256) void k_estep_final(unsigned long long* __restrict__ acc,
+                                                     double* __restrict__ out) {
+    __shared__ double vsum[kSlab];
+    finalize<false>(acc, vsum, out);
 }
 
 // cpg_counts_f64 from the 73 sums: init[8] trans[8][8] emit[8][4] loglik; thread t < 105
@@ -702,6 +656,7 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
 
 }  // namespace
 
+// accumulators | done counter (in the 1 KiB tail)
 size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep + 1024; }
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
@@ -716,8 +671,11 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
         const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long) +
                            (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
         if (!gtab) return hipErrorInvalidValue;   // est_tables
+        unsigned int* done =
+            parts == PART_ALL ? reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep) : nullptr;
         hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
-                           packed, C, acc, gtab);
+                           packed, C, acc, gtab, done, out);
+        if (done) return hipGetLastError();
     }
     if (parts & PART_FINAL)
         hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);

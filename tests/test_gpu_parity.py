@@ -453,3 +453,30 @@ def test_estep_trained_model_iteration(gpu_ctx, torch_dev):
         mg = co.normalize(D.bw_estep(gpu_ctx, _model(mg), dp, N, TRAIN).cpu().numpy())
         mo = co.normalize(co.estep(mo, obs, TRAIN))
     assert np.allclose(mg, mo, rtol=1e-8, atol=0)
+
+
+def test_estep_single_class_chunks(gpu_ctx, torch_dev):
+    """Chunks whose positions are (nearly) all one dinucleotide class: the per-chunk class
+    count the kernel recovers from its raw fixed-point bin sums (k_estep.hip class_count)
+    is then at its largest (65,535 for all-A) — parity with the oracle holds as elsewhere."""
+    from cpgisland_amd import device as D
+    n = 4 * TRAIN
+    cases = {
+        "allA": np.zeros(n, np.uint8),
+        "cg": np.tile(np.array([1, 2], np.uint8), n // 2),
+        "allT_then_random": np.concatenate(
+            [np.full(2 * TRAIN, 3, np.uint8),
+             np.random.default_rng(5).integers(0, 4, 2 * TRAIN).astype(np.uint8)]),
+    }
+    m = co.initial_model()
+    for name, obs in cases.items():
+        dp, _ = _dev_genome(pr.pack(obs), np.zeros(n // 32, np.uint32), torch_dev)
+        got = D.bw_estep(gpu_ctx, _model(m), dp, n, TRAIN).cpu().numpy()
+        ref = co.estep(m, obs, TRAIN)
+        nz = ref != 0
+        assert np.all(got[~nz] == 0), name
+        # bins whose expected count is below the fixed-point grid's reach (2^-47 per
+        # position, summed) are compared absolutely
+        big = nz & (np.abs(ref) > 1e-3)
+        assert np.max(np.abs(got[big] - ref[big]) / np.abs(ref[big])) < ESTEP_RTOL, name
+        assert np.max(np.abs(got[nz & ~big] - ref[nz & ~big]), initial=0.0) < 1e-9, name
