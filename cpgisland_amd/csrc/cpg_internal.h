@@ -70,17 +70,34 @@ struct __attribute__((aligned(8))) VitPlan {
 // counts last reads the accumulators with device-scope loads.  No L2 writeback fence is
 // needed (the only data exchanged is atomics): a release per workgroup would write back the
 // XCD's L2, including what concurrent kernels on the other stream have written.
+// The count is two-level: one device-scope word takes ~88 returning atomics per us, so 512
+// workgroups finishing together would queue ~6 us on a single counter; workgroup b counts
+// into group word b % kDoneGroups, and the last of each group into the top word
+// done[kDoneGroups].  The finalizer re-zeroes all of them (kDoneWords u32 of workspace).
+constexpr int kDoneGroups = 16;
+constexpr int kDoneWords = kDoneGroups + 1;
 #ifdef __HIPCC__
 __device__ __forceinline__ bool last_workgroup(unsigned int* done, int* s_flag) {
     __builtin_amdgcn_s_waitcnt(0);   // this wave's atomics have completed
     __syncthreads();
     if (threadIdx.x == 0) {
-        const unsigned prev =
-            __hip_atomic_fetch_add(done, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        *s_flag = prev == gridDim.x - 1;
+        const unsigned G = gridDim.x, g = blockIdx.x % kDoneGroups;
+        const unsigned gsize = (G - g + kDoneGroups - 1) / kDoneGroups;
+        bool last = false;
+        if (__hip_atomic_fetch_add(done + g, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) ==
+            gsize - 1) {
+            const unsigned ngroups = G < kDoneGroups ? G : kDoneGroups;
+            last = __hip_atomic_fetch_add(done + kDoneGroups, 1u, __ATOMIC_RELAXED,
+                                          __HIP_MEMORY_SCOPE_AGENT) == ngroups - 1;
+        }
+        *s_flag = last;
     }
     __syncthreads();
     return *s_flag != 0;
+}
+__device__ __forceinline__ void reset_done(unsigned int* done) {
+    if (threadIdx.x < kDoneWords)
+        __hip_atomic_store(done + threadIdx.x, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);

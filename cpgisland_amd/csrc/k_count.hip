@@ -189,7 +189,7 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
     __shared__ uint64_t raw[kRaw];
     if (done && last_workgroup(done, &s_last)) {
         finalize<true>(gacc, raw, out);
-        if (threadIdx.x == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        reset_done(done);
     }
 }
 
@@ -275,6 +275,7 @@ hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nc
     return hipGetLastError();
 }
 
-size_t count_ws_bytes(int64_t) { return (size_t)kRaw * 8 * kCntRep + 64; }   // + done counter
+// + the done counters
+size_t count_ws_bytes(int64_t) { return (size_t)kRaw * 8 * kCntRep + 4 * kDoneWords; }
 
 }  // namespace cpg

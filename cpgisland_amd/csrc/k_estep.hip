@@ -582,7 +582,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     // done != nullptr: the last workgroup to finish converts the sums (one launch per call)
     if (done && last_workgroup(done, reinterpret_cast<int*>(part))) {
         finalize<true>(acc, reinterpret_cast<double*>(part + 2), out);
-        if (t == 0) __hip_atomic_store(done, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        reset_done(done);
     }
 #ifdef CPG_DEBUG_ESTEP
     if (t == 0 && (c == 0 || c == 300 || c == (int64_t)gridDim.x - 1))

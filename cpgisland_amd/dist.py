@@ -14,10 +14,26 @@ whole decode chunks needs no data-path exchange at all:
                          (cpg_islands_at_d)
   * ShardRunner          the per-rank training pass + decode on that rank's device
 
+Shards need not be chunk-aligned: with boundaries at any multiple of 64 bases (an even split
+of a genome, shard_bounds(..., align=64)), every chunk is processed by the rank that holds its
+first base, and a chunk that runs past the end of that rank's shard is completed with the
+next rank's first bases — one all-gather of every rank's first 2^20 bases (packed + sign words,
+384 KB per rank), the halo:
+
+  * shard_plan()         the chunks a rank owns and the base range its local buffer covers
+  * halo_exchange()      the all-gather; returns the next rank's head
+  * local_buffers()      the rank's own words from its first owned chunk + the halo
+  * HaloShardRunner      ShardRunner over such a shard
+
+Every chunk is then computed whole, on one device, by the same kernels as the unsharded run:
+counts, island records and decoded paths are bit-identical to it for any shard boundaries.
+
 Backend "nccl" is RCCL over xGMI on the GPU box; "gloo" runs the same code on CPU tensors
 (tests/test_dist.py).  All messages are < 1 KiB except the island gather.
 """
 from __future__ import annotations
+
+from dataclasses import dataclass
 
 import numpy as np
 import torch
@@ -116,5 +132,137 @@ class ShardRunner:
         sign, score = D.viterbi(self.ctx, model, self.packed, self.n)
         out, cnt = D.islands(self.ctx, self.packed, sign, self.n, cap=cap,
                              first_chunk=self.start // _lib.DECODE_CHUNK)
+        isl = D.islands_to_numpy(out, cnt)
+        return sign, score, gather_islands(isl, self.packed.device, self.group)
+
+
+# ---------------------------------------------------------------- unaligned shards (halo)
+HALO_ALIGN = 64   # shard boundaries: whole sign words (32 bases) and count blocks (64 bases)
+
+
+def chunk_span(start: int, n: int, nbases: int, chunk: int) -> tuple[int, int]:
+    """Indices [c0, c1) of the whole `chunk`-base chunks of a genome of `nbases` bases (the
+    reference drops the tail) whose first base lies in [start, start + n)."""
+    last = nbases // chunk
+    c0 = min(-(-start // chunk), last)
+    c1 = min(-(-(start + n) // chunk), last)
+    return c0, max(c0, c1)
+
+
+@dataclass(frozen=True)
+class ShardPlan:
+    start: int      # the shard: bases [start, start + n) of the genome
+    n: int
+    t0: int         # owned training chunks [t0, t1) and decode chunks [d0, d1)
+    t1: int
+    d0: int
+    d1: int
+    base: int       # the local buffer: bases [base, end)
+    end: int
+    train: int
+    decode: int
+
+    @property
+    def halo(self) -> int:
+        """Bases past the shard's end that its last chunk needs (from the next rank)."""
+        return max(0, self.end - (self.start + self.n))
+
+
+def shard_plan(start: int, n: int, nbases: int, train: int = _lib.TRAIN_CHUNK,
+               decode: int = _lib.DECODE_CHUNK) -> ShardPlan:
+    if start % HALO_ALIGN or (start + n < nbases and n % HALO_ALIGN) or decode % train:
+        raise ValueError("shard boundaries must be multiples of 64 bases; decode chunk a "
+                         "multiple of the training chunk")
+    t0, t1 = chunk_span(start, n, nbases, train)
+    d0, d1 = chunk_span(start, n, nbases, decode)
+    firsts = ([t0 * train] if t1 > t0 else []) + ([d0 * decode] if d1 > d0 else [])
+    ends = ([t1 * train] if t1 > t0 else []) + ([d1 * decode] if d1 > d0 else [])
+    base = min(firsts) if firsts else start
+    end = max(ends) if ends else base
+    return ShardPlan(start, n, t0, t1, d0, d1, base, end, train, decode)
+
+
+def halo_exchange(packed: torch.Tensor, sign: torch.Tensor, n: int, group=None,
+                  width: int = _lib.DECODE_CHUNK):
+    """All-gather of every rank's first `width` bases (packed and sign words, zero-padded);
+    returns the next rank's (packed head, sign head), or (None, None) on the last rank."""
+    ws = _group_size(group)
+    if ws == 1:
+        return None, None
+    rank = dist.get_rank(group)
+    w16, w32 = width // 16, width // 32
+    hp = torch.zeros(w16, dtype=packed.dtype, device=packed.device)
+    hs = torch.zeros(w32, dtype=sign.dtype, device=sign.device)
+    k16, k32 = min(w16, (n + 15) // 16), min(w32, (n + 31) // 32)
+    hp[:k16] = packed[:k16]
+    hs[:k32] = sign[:k32]
+    gp = [torch.empty_like(hp) for _ in range(ws)]
+    gs = [torch.empty_like(hs) for _ in range(ws)]
+    dist.all_gather(gp, hp, group=group)
+    dist.all_gather(gs, hs, group=group)
+    if rank == ws - 1:
+        return None, None
+    return gp[rank + 1], gs[rank + 1]
+
+
+def local_buffers(packed: torch.Tensor, sign: torch.Tensor, plan: ShardPlan,
+                  head_p: torch.Tensor | None, head_s: torch.Tensor | None):
+    """The rank's packed / sign words of bases [plan.base, plan.end): its own words from
+    plan.base, then the halo from the next rank's head (padded by 4 words, as the kernels'
+    buffers are)."""
+    if plan.halo and (head_p is None or plan.halo > head_p.numel() * 16):
+        raise ValueError("the halo reaches past the next rank's head: shards must hold at "
+                         "least one decode chunk")
+    off = plan.base - plan.start
+    own = min(plan.start + plan.n, plan.end) - plan.base
+    if own < 0 or off < 0:
+        raise ValueError("bad shard plan")
+    p = [packed[off // 16: off // 16 + (own + 15) // 16]]
+    s = [sign[off // 32: off // 32 + (own + 31) // 32]]
+    if plan.halo:
+        p.append(head_p[: (plan.halo + 15) // 16])
+        s.append(head_s[: (plan.halo + 31) // 32])
+    pad_p = torch.zeros(4, dtype=packed.dtype, device=packed.device)
+    pad_s = torch.zeros(4, dtype=sign.dtype, device=sign.device)
+    return torch.cat(p + [pad_p]), torch.cat(s + [pad_s])
+
+
+class HaloShardRunner:
+    """ShardRunner over a shard with boundaries at any multiple of 64 bases: the chunks whose
+    first base the shard holds, each computed whole (with the halo from the next rank)."""
+
+    def __init__(self, ctx, packed: torch.Tensor, sign: torch.Tensor, start: int, n: int,
+                 nbases: int, group=None, heads=None):
+        self.ctx, self.group = ctx, group
+        self.plan = shard_plan(start, n, nbases)
+        hp, hs = heads if heads is not None else halo_exchange(packed, sign, n, group)
+        self.packed, self.sign = local_buffers(packed, sign, self.plan, hp, hs)
+
+    def _train_view(self):
+        pl = self.plan
+        o = pl.t0 * pl.train - pl.base
+        return (self.packed[o // 16:], self.sign[o // 32:], (pl.t1 - pl.t0) * pl.train)
+
+    def labelled_counts(self) -> torch.Tensor:
+        from . import device as D
+        p, s, n = self._train_view()
+        return merge_counts_i64(D.count_labelled(self.ctx, p, s, n), self.group)
+
+    def estep(self, model) -> np.ndarray:
+        from . import device as D
+        p, _, n = self._train_view()
+        return merge_counts_f64(D.bw_estep(self.ctx, model, p, n), self.group).cpu().numpy()
+
+    def decode(self, model, cap: int = 1 << 20):
+        """Exact Viterbi of the owned decode chunks + island scan with global chunk numbers;
+        returns (sign tensor of the owned chunks, scores, all ranks' islands in genome
+        order)."""
+        from . import device as D
+        pl = self.plan
+        o = pl.d0 * pl.decode - pl.base
+        p = self.packed[o // 16:]
+        n = (pl.d1 - pl.d0) * pl.decode
+        sign, score = D.viterbi(self.ctx, model, p, n)
+        out, cnt = D.islands(self.ctx, p, sign, n, cap=cap, first_chunk=pl.d0)
         isl = D.islands_to_numpy(out, cnt)
         return sign, score, gather_islands(isl, self.packed.device, self.group)

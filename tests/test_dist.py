@@ -126,3 +126,79 @@ def test_single_process_merges_are_identity():
     assert cd.merge_counts_i64(t.long()).equal(t.long())
     with pytest.raises(ValueError):
         cd.shard_bounds(10, 2, 2)
+
+
+# ---------------------------------------------------------------- unaligned shards (halo)
+def _halo_worker(rank, world, port, q):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        obs, truth = _genome()
+        start, n = cd.shard_bounds(N, world, rank, align=cd.HALO_ALIGN)
+        # this rank's own words only (its first base at bit 0), as a loader would produce them
+        pk = torch.from_numpy(pr.pack(obs[start:start + n]).view(np.int32).copy())
+        sg = torch.from_numpy(pr.pack_bits(truth[start:start + n]).view(np.int32).copy())
+        plan = cd.shard_plan(start, n, N, train=TRAIN, decode=DECODE)
+        hp, hs = cd.halo_exchange(pk, sg, n, width=DECODE)
+        lp, ls = cd.local_buffers(pk, sg, plan, hp, hs)
+        span = plan.end - plan.base
+        lo = pr.unpack(lp.numpy().view(np.uint32), span)
+        lt = pr.unpack_bits(ls.numpy().view(np.uint32), span)
+        # the local buffer IS the genome's bases [base, end): halo included
+        assert np.array_equal(lo, obs[plan.base:plan.end])
+        assert np.array_equal(lt, truth[plan.base:plan.end])
+        m = co.initial_model()
+        to, tn = plan.t0 * TRAIN - plan.base, (plan.t1 - plan.t0) * TRAIN
+        li = cd.merge_counts_i64(torch.from_numpy(
+            co.count_labelled(lo[to:to + tn], lt[to:to + tn], TRAIN)))
+        fe = cd.merge_counts_f64(torch.from_numpy(co.estep(m, lo[to:to + tn], TRAIN)))
+        do = plan.d0 * DECODE - plan.base
+        recs = [co.islands(co.viterbi8(m, lo[do + c * DECODE:do + (c + 1) * DECODE])[0],
+                           plan.d0 + c) for c in range(plan.d1 - plan.d0)]
+        isl = np.concatenate(recs) if recs else np.zeros(0, co.ISLAND_DTYPE)
+        gi = cd.gather_islands(isl.view(_lib.ISLAND_DTYPE), torch.device("cpu"))
+        q.put((rank, start, n, plan.halo, li.numpy(), fe.numpy(), gi.view(np.uint8).copy()))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_unaligned_shards_with_halo_equal_unsharded(world):
+    """Shards split at multiples of 64 bases (not at chunk boundaries): every chunk is run by
+    the rank holding its first base, completed by the halo all-gather — counts and island
+    records equal the unsharded run's."""
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_halo_worker, args=(world, _free_port(), q), nprocs=world, join=True,
+                       start_method="spawn")
+    res = sorted([q.get() for _ in range(world)], key=lambda r: r[0])
+    obs, truth = _genome()
+    assert sum(r[2] for r in res) == N
+    assert any(r[1] % DECODE for r in res)       # really unaligned
+    assert any(r[3] > 0 for r in res)            # some chunk needed the halo
+    full_i = co.count_labelled(obs, truth, TRAIN)
+    m = co.initial_model()
+    full_e = co.estep(m, obs, TRAIN)
+    _, isl, _ = co.decode_chunks(m, obs, DECODE)
+    nz = full_e != 0
+    for r in res:
+        assert np.array_equal(r[4], full_i)
+        assert np.array_equal(r[5], res[0][5])
+        assert np.max(np.abs(r[5][nz] - full_e[nz]) / np.abs(full_e[nz])) < 1e-12
+        assert np.array_equal(r[6].view(co.ISLAND_DTYPE), isl)
+
+
+@pytest.mark.parametrize("n,world", [(5 * DECODE + 1234, 2), (5 * DECODE + 1234, 4),
+                                     (3_100_000_000, 8)])
+def test_shard_plans_cover_every_chunk_once(n, world):
+    plans = [cd.shard_plan(*cd.shard_bounds(n, world, r, align=cd.HALO_ALIGN), n)
+             for r in range(world)]
+    for a, b in zip(plans, plans[1:]):
+        assert a.t1 == b.t0 and a.d1 == b.d0       # chunk ranges tile
+        assert a.halo <= b.n                        # the halo is inside the next shard
+    assert plans[0].t0 == 0 and plans[-1].t1 == n // _lib.TRAIN_CHUNK
+    assert plans[0].d0 == 0 and plans[-1].d1 == n // _lib.DECODE_CHUNK
+    for p in plans:
+        assert p.halo < _lib.DECODE_CHUNK
+    with pytest.raises(ValueError):
+        cd.shard_plan(100, 64, n)                   # not a multiple of 64

@@ -480,3 +480,22 @@ def test_estep_single_class_chunks(gpu_ctx, torch_dev):
         big = nz & (np.abs(ref) > 1e-3)
         assert np.max(np.abs(got[big] - ref[big]) / np.abs(ref[big])) < ESTEP_RTOL, name
         assert np.max(np.abs(got[nz & ~big] - ref[nz & ~big]), initial=0.0) < 1e-9, name
+
+
+def test_fused_finalize_across_grid_sizes(gpu_ctx, torch_dev):
+    """The count and E-step launches finalize in their last workgroup (two-level done
+    counters, re-zeroed by the finalizer): calls of every grid size — fewer workgroups than
+    counter groups, more, uneven groups — in any order each return their own sums."""
+    from cpgisland_amd import device as D
+    m = co.initial_model()
+    packed, sign = D.synth_host(123, 0, 41 * TRAIN)
+    obs, truth = pr.unpack(packed, 41 * TRAIN), pr.unpack_bits(sign, 41 * TRAIN)
+    dp, ds = _dev_genome(packed, sign, torch_dev)
+    for nch in [2, 17, 41, 9, 1, 41, 2, 33]:
+        n = nch * TRAIN + (nch % 3) * 100
+        e = D.bw_estep(gpu_ctx, _model(m), dp, n, TRAIN).cpu().numpy()
+        ref = co.estep(m, obs[:n], TRAIN)
+        nz = ref != 0
+        assert np.max(np.abs(e[nz] - ref[nz]) / np.abs(ref[nz])) < ESTEP_RTOL, nch
+        c = D.count_labelled(gpu_ctx, dp, ds, n, TRAIN).cpu().numpy()
+        assert np.array_equal(c, co.count_labelled(obs[:n], truth[:n], TRAIN)), nch
