@@ -262,10 +262,13 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 #else
 #define CPG_EST_MARK(n)
 #endif
-// waves per SIMD: 4 (123 VGPRs, no spills).  5 (<= 96 VGPRs, 23 spilled) was measured so that
-// decode waves could share the training CUs: 208 vs 218-224 Gbase/s (r01_v10 A/B), rejected.
+// waves per SIMD: the workgroup's 16 waves take 4 per SIMD; with <= 96 VGPRs (5 per SIMD) a
+// fifth wave slot and 128 VGPRs per SIMD stay free for the decode stream's kernels, whose
+// latency-bound waves then fill this kernel's idle issue slots (overlapped bench +3-4 %,
+// tools/ab_libs.sh; a few spills, none of them in the main loop's steady state).  At 4 per
+// SIMD (122 VGPRs, no spills) the kernel alone is as fast; 6 per SIMD spills 38.
 #ifndef CPG_EST_WPE
-#define CPG_EST_WPE 4
+#define CPG_EST_WPE 5
 #endif
 __global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(CPG_EST_WPE)))
 void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
@@ -469,25 +472,36 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
             bfP = f.x;
             bfM = f.y;
         }
-        double alP[kMB], alM[kMB];
+        // alpha registers hold one half of the mini-block: the second half's alphas from a
+        // forward pass over all 16 positions, then (after its backward pass) the first half's
+        // from a second forward pass — 32 fewer VGPRs than the whole mini-block's, for 2 extra
+        // fp64 per position, so that the kernel fits 5 waves per SIMD (see CPG_EST_WPE)
+        constexpr int kH = kMB / 2;
+        double alP[kH], alM[kH];
+        double hP = bfP, hM = bfM;   // alpha at position lo - 1 (the position before the half)
         int kf[kMB / 4];   // alpha's power-of-two shifts at positions 3, 7, 11, 15
-        double xP = bfP, xM = bfM;
+        auto forward = [&](int lo, int hi) {   // positions [0, hi); alphas of [lo, hi) kept
+            double xP = bfP, xM = bfM;
 #pragma unroll
-        for (int i = 0; i < kMB; ++i) {
-            if (t == 0 && m == 0 && i == 0) {   // alpha_0 itself
-                alP[i] = xP;
-                alM[i] = xM;
-                continue;
+            for (int i = 0; i < hi; ++i) {
+                if (!(t == 0 && m == 0 && i == 0)) {   // (alpha_0 itself at the chunk start)
+                    const uint32_t d = code_at(cm, i);
+                    const double2 ma = TA[d], mb = TB[d];
+                    const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
+                    xP = nP;
+                    xM = nM;
+                    if ((i & 3) == 3) kf[i >> 2] = vnorm(xP, xM);
+                }
+                if (i == lo - 1) {
+                    hP = xP;
+                    hM = xM;
+                }
+                if (i >= lo) {
+                    alP[i - lo] = xP;
+                    alM[i - lo] = xM;
+                }
             }
-            const uint32_t d = code_at(cm, i);
-            const double2 ma = TA[d], mb = TB[d];
-            const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
-            xP = nP;
-            xM = nM;
-            if ((i & 3) == 3) kf[i >> 2] = vnorm(xP, xM);
-            alP[i] = xP;
-            alM[i] = xM;
-        }
+        };
         // beta pre-scaled by 2^47 / Z: with a_i = the stored (renormalised) alpha at i and
         // s_i its shift (a_{i-1} M_i = 2^{s_i} a_i), keep  a_{i-1} . (M_i y_i) = 2^47  at
         // every position, so xi_i(a,b) * 2^47 = a_{i-1}(a) * (M_i(a,b) y_i(b)) — one fma per
@@ -496,56 +510,66 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         // alpha renormalisation point going backward (i-1 = 11, 7, 3) scales y by 2^{-s}.
         // y only shrinks through M (entries <= 1) and grows by the alpha shifts of one
         // mini-block; it is renormalised once per mini-block.
-        vnorm(yP, yM);
-        {
-            const double r = ldexp(rcp_nr(alP[kMB - 1] * yP + alM[kMB - 1] * yM), 47 - kf[3]);
+        auto bstart = [&]() {
+            vnorm(yP, yM);
+            const double r =
+                ldexp(rcp_nr(alP[kH - 1] * yP + alM[kH - 1] * yM), 47 - kf[kMB / 4 - 1]);
             yP *= r;
             yM *= r;
-        }
+        };
 #ifndef EST_PFD
 #define EST_PFD 1   // backward table rows loaded this many positions ahead (2, 3: no faster)
 #endif
         // the backward pass's table rows come from a global copy (L1-resident): waited on
         // with vmcnt, not behind the preceding LDS atomics (LDS operations retire in order;
         // an LDS copy read ahead of the atomics spills)
-        double2 qa[EST_PFD + 1], qb[EST_PFD + 1];
-        auto trow = [&](int i, double2& a, double2& b) {
-            const uint32_t d = code_at(cm, i);
-            a = gtab[d];
-            b = gtab[16 + d];
+        auto backward = [&](int lo, int hi) {   // positions hi - 1 .. lo
+            double2 qa[EST_PFD + 1], qb[EST_PFD + 1];
+            auto trow = [&](int i, double2& a, double2& b) {
+                const uint32_t d = code_at(cm, i);
+                a = gtab[d];
+                b = gtab[16 + d];
+            };
+#pragma unroll
+            for (int j = 0; j < EST_PFD; ++j) trow(hi - 1 - j, qa[j], qb[j]);
+#pragma unroll
+            for (int i = hi - 1; i >= lo; --i) {
+                // table rows issued EST_PFD positions ahead; the scheduling barrier keeps the
+                // compiler from sinking them to their use, which had put one full L1/L2 round
+                // trip (two, serialised) on every position's chain
+                if (i - EST_PFD >= lo)
+                    trow(i - EST_PFD, qa[(hi - 1 - i + EST_PFD) % (EST_PFD + 1)],
+                         qb[(hi - 1 - i + EST_PFD) % (EST_PFD + 1)]);
+                __builtin_amdgcn_sched_barrier(0);
+                const uint32_t d = code_at(cm, i);
+                const double2 ma = qa[(hi - 1 - i) % (EST_PFD + 1)],
+                              mb = qb[(hi - 1 - i) % (EST_PFD + 1)];
+                if (t == 0 && m == 0 && i == 0) {   // gamma_0 = a_0 * y_0 / 2^47 -> init counts
+                    g0P = alP[0] * yP;
+                    g0M = alM[0] * yM;
+                    continue;
+                }
+                const double uP = i > lo ? alP[i - 1 - lo] : (lo > 0 ? hP : bfP);
+                const double uM = i > lo ? alM[i - 1 - lo] : (lo > 0 ? hM : bfM);
+                // M y products, shared by the pair marginals and the beta update
+                const double t00 = ma.x * yP, t01 = ma.y * yM, t10 = mb.x * yP, t11 = mb.y * yM;
+                atomicAdd(wb + bin_of(d, 0) * kBS, raw_fma(uP, t00));
+                atomicAdd(wb + bin_of(d, 1) * kBS, raw_fma(uP, t01));
+                atomicAdd(wb + bin_of(d, 2) * kBS, raw_fma(uM, t10));
+                atomicAdd(wb + bin_of(d, 3) * kBS, raw_fma(uM, t11));
+                yP = t00 + t01;
+                yM = t10 + t11;
+                if (i == 4 || i == 8 || i == 12) {
+                    yP = ldexp(yP, -kf[(i - 1) >> 2]);
+                    yM = ldexp(yM, -kf[(i - 1) >> 2]);
+                }
+            }
         };
-#pragma unroll
-        for (int j = 0; j < EST_PFD; ++j) trow(kMB - 1 - j, qa[j], qb[j]);
-#pragma unroll
-        for (int i = kMB - 1; i >= 0; --i) {
-            // table rows issued EST_PFD positions ahead; the scheduling barrier keeps the
-            // compiler from sinking them to their use, which had put one full L1/L2 round trip
-            // (two, serialised) on every position's chain
-            if (i - EST_PFD >= 0) trow(i - EST_PFD, qa[(kMB - 1 - i + EST_PFD) % (EST_PFD + 1)],
-                                       qb[(kMB - 1 - i + EST_PFD) % (EST_PFD + 1)]);
-            __builtin_amdgcn_sched_barrier(0);
-            const uint32_t d = code_at(cm, i);
-            const double2 ma = qa[(kMB - 1 - i) % (EST_PFD + 1)], mb = qb[(kMB - 1 - i) % (EST_PFD + 1)];
-            if (t == 0 && m == 0 && i == 0) {   // gamma_0 = a_0 * y_0 / 2^47 -> init counts
-                g0P = alP[0] * yP;
-                g0M = alM[0] * yM;
-                continue;
-            }
-            const double uP = i > 0 ? alP[i - 1] : bfP;
-            const double uM = i > 0 ? alM[i - 1] : bfM;
-            // M y products, shared by the pair marginals and the beta update
-            const double t00 = ma.x * yP, t01 = ma.y * yM, t10 = mb.x * yP, t11 = mb.y * yM;
-            atomicAdd(wb + bin_of(d, 0) * kBS, raw_fma(uP, t00));
-            atomicAdd(wb + bin_of(d, 1) * kBS, raw_fma(uP, t01));
-            atomicAdd(wb + bin_of(d, 2) * kBS, raw_fma(uM, t10));
-            atomicAdd(wb + bin_of(d, 3) * kBS, raw_fma(uM, t11));
-            yP = t00 + t01;
-            yM = t10 + t11;
-            if (i == 4 || i == 8 || i == 12) {
-                yP = ldexp(yP, -kf[(i - 1) >> 2]);
-                yM = ldexp(yM, -kf[(i - 1) >> 2]);
-            }
-        }
+        forward(kH, kMB);
+        bstart();
+        backward(kH, kMB);
+        forward(0, kH);
+        backward(0, kH);
     }
     __syncthreads();
     CPG_EST_MARK(T6)
