@@ -32,6 +32,13 @@ SHARD_STRIDE = 44 << 20        # 1 Mi-aligned shard starts (44 decode chunks >= 
 TRAIN = 65536
 DECODE = 1 << 20
 HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
+# fp64 vector peak of the MI355X (AMD's published 78.6 TFLOP/s: 256 CUs x 2.4 GHz x 128 fp64
+# flops per clock; the guides give no fp64 figure) and the E-step's ALGORITHMIC fp64 flops
+# per base (FMA = 2): forward alpha 2 mul + 2 fma = 6, backward 4 mul + 4 fma + 2 add = 14,
+# lane products 4 two-by-two products per 16 positions = 3 — implementation recomputation
+# (the second forward pass over half of each mini-block) not counted
+FP64_PEAK_TFLOPS = 78.6
+ESTEP_FLOPS_PER_BASE = 23
 # algorithmic bytes per base of each phase
 BYTES_PER_BASE = {"estep": 0.25, "counts": 0.375, "viterbi": 0.375, "islands": 0.375}
 
@@ -430,6 +437,13 @@ def main():
         roof["limiter"] = "fp64 VALU issue + dependency latency, not HBM (PMC: profiles/*pmc*)"
         roof["note"] = ("exact fp64 forward-backward: ~50 VALU instructions per base against "
                         "0.25 B/base of HBM traffic; DESIGN.md 5")
+        # the limiter named above, priced: algorithmic fp64 flops per launch / the same phase
+        # time, against the fp64 vector peak
+        fl = ESTEP_FLOPS_PER_BASE * N / (phases[dom] / 1e3) / 1e12 if phases[dom] > 0 else 0.0
+        roof_fp64 = {"bound": "valu-fp64", "kernel": "k_estep_chunk", "phase": dom,
+                     "achieved": round(fl, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(fl / FP64_PEAK_TFLOPS, 4),
+                     "flops_per_base": ESTEP_FLOPS_PER_BASE}
         vit = phases["viterbi"] + phases["islands"] if full_ev else phases["decode"]
         roof_decode = {"phase": "viterbi+islands", "achieved": round(
             (BYTES_PER_BASE["viterbi"] + BYTES_PER_BASE["islands"]) * N / (vit / 1e3) / 1e9
@@ -465,7 +479,7 @@ def main():
                                            sum(int(p["icnt"].item()) for p in lanes[0]["parts"])},
                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
                "host_issue_ms_per_step": round(issue * 1e3 / steps, 4),
-               "roofline": roof, "roofline_decode": roof_decode,
+               "roofline": roof, "roofline_fp64": roof_fp64, "roofline_decode": roof_decode,
                "cold_cache": cold}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(SEED, args.cpu_sample,

@@ -456,6 +456,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     constexpr int kBS = 16;   // row stride
     double g0P = 0.0, g0M = 0.0;
     double yP = bP, yM = bM;   // beta at the last position of the mini-block
+#ifdef CPG_STAMP_ESTEP
+    unsigned long long st_f1 = 0, st_b1 = 0, st_f2 = 0, st_b2 = 0;
+#endif
     // (measured and dropped: mini-block m's backward pass interleaved with mini-block m-1's
     // forward pass, two dependency chains per wave — 16 alpha pairs live either way, but the
     // two chains' temporaries spill: 0.18 vs 0.127 ms)
@@ -565,12 +568,40 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
                 }
             }
         };
+#if defined(CPG_STAMP_ESTEP)   // diagnostic build: shader-clock cycles per pass
+
+#define EST_STAMP(v)                                                                   \
+    __builtin_amdgcn_sched_barrier(0);                                                 \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");          \
+    __builtin_amdgcn_sched_barrier(0);
+        unsigned long long s0, s1, s2, s3, s4;
+        EST_STAMP(s0)
+        forward(kH, kMB);
+        EST_STAMP(s1)
+        bstart();
+        backward(kH, kMB);
+        EST_STAMP(s2)
+        forward(0, kH);
+        EST_STAMP(s3)
+        backward(0, kH);
+        EST_STAMP(s4)
+        st_f1 += s1 - s0;
+        st_b1 += s2 - s1;
+        st_f2 += s3 - s2;
+        st_b2 += s4 - s3;
+#else
         forward(kH, kMB);
         bstart();
         backward(kH, kMB);
         forward(0, kH);
         backward(0, kH);
+#endif
     }
+#ifdef CPG_STAMP_ESTEP
+    if (lane == 0 && (c == 0 || c == 300 || c == 700) && (t >> 6) % 5 == 0)
+        printf("stamp c%lld w%d: fwd16 %llu bwd8 %llu fwd8 %llu bwd8 %llu (cycles, 4 mini-blocks)\n",
+               (long long)c, t >> 6, st_f1, st_b1, st_f2, st_b2);
+#endif
     __syncthreads();
     CPG_EST_MARK(T6)
     // chunk totals: row t = d * 4 + k, the sum of its 16 columns (integer: exact in any order)
