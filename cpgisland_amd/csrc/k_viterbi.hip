@@ -37,6 +37,7 @@
 // Layout: packed bases (16/uint32, base k at bits 2k), sign bits (32/uint32), all in HBM.
 // Dinucleotide code d = prev | cur << 2 (one bfe of the packed word).
 
+#include <algorithm>
 #include <cfloat>
 #include <cmath>
 
@@ -271,10 +272,12 @@ __device__ void vit_head(const VitConsts& vc, const uint32_t* packed, const Geo&
 // model only; k_vit_tables writes them once per model (vit_tables' cache) right after the
 // VitTables in the same allocation, and every K1/K3 workgroup copies its part to LDS.
 constexpr int kQ4 = 1280;   // 4-step products over 5-base windows [0, 1024), 3-step [1024, 1280)
+constexpr int kW4 = 1024;   // 4-step composites over 5-base windows b0..b4 (bits 2k: b_k)
 struct VitDerived {
     int4 Q4[kQ4];
     double2 sA[kMaxBinade * 16], sB[kMaxBinade * 16];    // single-step halves (l0,l1) | (l2,l3)
     double2 P2A[kMaxBinade * 64], P2B[kMaxBinade * 64];  // 2-step composites (pp,pm) | (mp,mm)
+    double2 P4A[kMaxBinade * kW4], P4B[kMaxBinade * kW4];   // 4-step composites, same halves
 };
 __device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
     return reinterpret_cast<const VitDerived*>(vt + 1);
@@ -282,7 +285,7 @@ __device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
 
 __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables* vt) {
     VitDerived* dv = reinterpret_cast<VitDerived*>(vt + 1);
-    const int n = kQ4 + kMaxBinade * 16 + kMaxBinade * 64;
+    const int n = kQ4 + kMaxBinade * 16 + kMaxBinade * 64 + kMaxBinade * kW4;
     for (int i = blockIdx.x * kThreads + threadIdx.x; i < n; i += gridDim.x * kThreads) {
         if (i < kQ4) {   // i >= 1024: 3-step entries (block 0's first window; b0 unused)
             const bool three = i >= 1024;
@@ -301,6 +304,17 @@ __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables
             const double* l = vt->Le[j / 16][j % 16];
             dv->sA[j] = make_double2(l[0], l[1]);
             dv->sB[j] = make_double2(l[2], l[3]);
+        } else if (i >= kQ4 + kMaxBinade * 16 + kMaxBinade * 64) {
+            // 4-step composite of window w: steps with dinucleotides (w >> 2k) & 15, k = 0..3
+            const int j = i - kQ4 - kMaxBinade * 16 - kMaxBinade * 64, e = j / kW4, w = j % kW4;
+            const double* l = vt->Le[e][w & 15];
+            C64 m{l[0], l[2], l[1], l[3]};
+            for (int k = 1; k < 4; ++k) {
+                const double* lk = vt->Le[e][(w >> (2 * k)) & 15];
+                c64_step(m, lk[0], lk[1], lk[2], lk[3]);
+            }
+            dv->P4A[j] = make_double2(m.pp, m.pm);
+            dv->P4B[j] = make_double2(m.mp, m.mm);
         } else {
             const int j = i - kQ4 - kMaxBinade * 16, e = j / 64, w = j % 64;
             const double* l1 = vt->Le[e][(w & 3) | (((w >> 2) & 3) << 2)];          // x -> y
@@ -522,38 +536,92 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     // per binade slot: single-step halves sA/sB [16] (one 256-B bank row each) and 2-step
     // composites over 3-base windows, halves P2A = (pp, pm), P2B = (mp, mm) [64].  Every
     // entry is a sum of binade-rounded constants: exact on the binade's grid.
+    // LDS: single-step halves of every binade [emin, emax] (partial blocks, the irregular
+    // blocks' workgroups), then a union: the 4-step composites of ONE binade (when every
+    // full REGULAR block of the workgroup lies in it: 64 lookups and max-plus products per
+    // block instead of 128) or the 2-step composites of every binade
     extern __shared__ __attribute__((aligned(16))) double2 sLe[];
     const int nb = vc.emax - vc.emin + 1;
     double2* sA = sLe;
     double2* sB = sA + nb * 16;
     double2* P2A = sB + nb * 16;
     double2* P2B = P2A + nb * 64;
-    {   // the binades [emin, emax] of the per-model tables (k_vit_tables)
-        const VitDerived* dv = derived(vt);
+    double2* P4A = sB + nb * 16;
+    double2* P4B = P4A + kW4;
+    __shared__ int s_emin, s_emax, s_part;
+    const VitDerived* dv = derived(vt);
+    auto load_single = [&]() {   // the single-step halves of every binade
         for (int i = threadIdx.x; i < nb * 16; i += kThreads) {
             sA[i] = dv->sA[vc.emin * 16 + i];
             sB[i] = dv->sB[vc.emin * 16 + i];
         }
+    };
+    if (blockIdx.x >= main_grid) {   // workgroup-uniform: the chunk's irregular blocks
+        load_single();
+        __syncthreads();
+        vit_irregular(vc, packed, g, aent, plan, irrlist, irrcount, comp3,
+                      (int64_t)(blockIdx.x - main_grid), sA, sB);
+        return;
+    }
+    if (threadIdx.x == 0) {
+        s_emin = 1 << 30;
+        s_emax = -(1 << 30);
+        s_part = 0;
+    }
+    __syncthreads();
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    const bool valid = gid < g.nchunks * g.nsb;
+    const VitPlan p = valid ? plan[gid] : VitPlan{PLAN_SEQ, 0, 0, 0, 0, 0};
+    const int64_t c = valid ? gid / g.nsb : 0, k = valid ? gid - c * g.nsb : 0;
+    const bool reg = valid && p.type == PLAN_REGULAR;
+    // a partial REGULAR block (the chunk's last, short one) walks single steps
+    if (reg && !g.full(k)) s_part = 1;
+    {   // binade range of the workgroup's full REGULAR blocks: wave reduction, one LDS atomic
+        int lo = (reg && g.full(k)) ? (int)p.e_pre : (1 << 30);
+        int hi = (reg && g.full(k)) ? (int)p.e_pre : -(1 << 30);
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) {
+            lo = min(lo, __shfl_xor(lo, off));
+            hi = max(hi, __shfl_xor(hi, off));
+        }
+        if ((threadIdx.x & 63) == 0) {
+            atomicMin(&s_emin, lo);
+            atomicMax(&s_emax, hi);
+        }
+    }
+    __syncthreads();
+    const bool four = s_emin == s_emax;   // workgroup-uniform
+    if (s_part) load_single();   // (tables only where a workgroup uses them: ~11 KB each)
+    if (four) {
+        const double2* ga = dv->P4A + (size_t)s_emin * kW4;
+        const double2* gb = dv->P4B + (size_t)s_emin * kW4;
+        for (int i = threadIdx.x; i < kW4; i += kThreads) {
+            P4A[i] = ga[i];
+            P4B[i] = gb[i];
+        }
+    } else {
         for (int i = threadIdx.x; i < nb * 64; i += kThreads) {
             P2A[i] = dv->P2A[vc.emin * 64 + i];
             P2B[i] = dv->P2B[vc.emin * 64 + i];
         }
     }
     __syncthreads();
-    if (blockIdx.x >= main_grid) {   // workgroup-uniform: the chunk's irregular blocks
-        vit_irregular(vc, packed, g, aent, plan, irrlist, irrcount, comp3,
-                      (int64_t)(blockIdx.x - main_grid), sA, sB);
-        return;
-    }
-    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (gid >= g.nchunks * g.nsb) return;
-    const VitPlan p = plan[gid];
-    if (p.type != PLAN_REGULAR) return;
-    const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
+    if (!reg) return;
     const uint32_t* pk = chunk_ptr(packed, g, c);
     const int slot = p.e_pre - vc.emin;
     C64 acc = c64_id();
-    if (g.full(k)) {
+    if (g.full(k) && four) {
+        const BlockWords bw = load_block(pk, k);
+        pipelined<4, 64>(
+            [&](int j) {   // 5-base window of steps 4j .. 4j+3
+                const int r = j >> 2, s = j & 3;
+                const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
+                return s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 0x3FFu)
+                              : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
+            },
+            [&](uint32_t wi) { return C64{P4A[wi].x, P4A[wi].y, P4B[wi].x, P4B[wi].y}; },
+            [&](const C64& m, int) { acc = c64_mul(acc, m); });
+    } else if (g.full(k)) {
         const double2* pa = P2A + slot * 64;
         const double2* pb = P2B + slot * 64;
         const BlockWords bw = load_block(pk, k);
@@ -1484,7 +1552,8 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                        w.comp1);
     hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks + head), dim3(kScanT), 0, s, vc, packed,
                        g, w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount, w.vhead);
-    const size_t lds3x = (size_t)(vc.emax - vc.emin + 1) * (16 + 64) * 2 * sizeof(double2);
+    const size_t nbz = (size_t)(vc.emax - vc.emin + 1);
+    const size_t lds3x = (nbz * 16 * 2 + std::max(nbz * 64 * 2, (size_t)kW4 * 2)) * sizeof(double2);
     // K3 + K3b in one launch: the chunks' irregular blocks run as extra workgroups
     hipLaunchKernelGGL(k_vit_exact, dim3(grid + (unsigned)nchunks), dim3(kThreads), lds3x, s, vc,
                        d_vt, packed, g, w.plan, w.comp3, status, grid, w.aent, w.splitlist,
@@ -1508,7 +1577,7 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
 size_t vit_derived_bytes() { return sizeof(VitDerived); }
 
 hipError_t launch_vit_tables(const VitConsts& vc, VitTables* d_vt, hipStream_t s) {
-    hipLaunchKernelGGL(k_vit_tables, dim3(24), dim3(kThreads), 0, s, vc, d_vt);
+    hipLaunchKernelGGL(k_vit_tables, dim3(128), dim3(kThreads), 0, s, vc, d_vt);
     return hipGetLastError();
 }
 
