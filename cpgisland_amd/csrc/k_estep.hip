@@ -412,10 +412,14 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     __syncthreads();
     const uint32_t o0 = pk[0] & 3u;
     const double fa = model.pi[o0], fb = model.pi[o0 + 4];   // alpha_0 (b = 1 when live)
-    double loglik = 0.0;
-    if (t == nl - 1) {
+    unsigned long long* racc = acc + 2 * kSlab * (c % kAccRep);
+    if (t == nl - 1) {   // the chunk log-likelihood, in signed 2^-24 units (added now: nothing
+                         // stays live across the main loop)
         const Mat A = sXP[16];
-        loglik = log(fa * (A.a + A.b) + fb * (A.c + A.d)) + (double)A.e * 0.69314718055994530942;
+        const double loglik =
+            log(fa * (A.a + A.b) + fb * (A.c + A.d)) + (double)A.e * 0.69314718055994530942;
+        const long long L = llrint(ldexp(loglik, kLogFix));
+        acc128_add(racc + 2 * 72, (unsigned long long)L, L < 0);
     }
     double aP = fa, aM = fb;   // alpha at position p0-1 (t > 0); alpha_0 for t == 0
     if (t > 0) {
@@ -432,8 +436,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     }
     vnorm(bP, bM);
     CPG_EST_MARK(T3)
-    // the alpha checkpoints (see 3a) of mini-blocks 1.. in LDS ([m-1][lane], 16-B rows:
-    // conflict-free), mini-block 0's is (aP, aM) itself: registers stay below 128
+    // the alpha checkpoints (see 3a) of mini-blocks 1.. in LDS ([m-1][lane], the first 16 B
+    // of each 32-B product slot: conflict-free rows); mini-block 0's, (aP, aM) itself, in the
+    // second half of slot [0][lane] (no register stays live across the main loop for it)
 #pragma unroll
     for (int m = 1; m < NMB; ++m) {
         const double4 A = fck4[(m - 1) * nl + t];
@@ -441,6 +446,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         vnorm(xP, xM);
         fck[2 * ((m - 1) * nl + t)] = make_double2(xP, xM);
     }
+    fck[2 * t + 1] = make_double2(aP, aM);
     __syncthreads();
     CPG_EST_MARK(T4)
 
@@ -454,7 +460,6 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     //     backward with xi accumulation; beta flows on from one mini-block to the previous
     unsigned long long* wb = bins + (lane & 15);
     constexpr int kBS = 16;   // row stride
-    double g0P = 0.0, g0M = 0.0;
     double yP = bP, yM = bM;   // beta at the last position of the mini-block
 #ifdef CPG_STAMP_ESTEP
     unsigned long long st_f1 = 0, st_b1 = 0, st_f2 = 0, st_b2 = 0;
@@ -468,13 +473,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         const uint32_t xw = pk[4 * t + m];
         const uint32_t pw = (t > 0 || m > 0) ? pk[4 * t + m - 1] : 0u;
         const uint64_t cm = codes16(xw, pw >> 30);
-        // alpha at the position before the mini-block (select chain: no register indexing)
-        double bfP = aP, bfM = aM;
-        if (m > 0) {
-            const double2 f = fck[2 * ((m - 1) * nl + t)];
-            bfP = f.x;
-            bfM = f.y;
-        }
+        // alpha at the position before the mini-block (its checkpoint)
+        const double2 f = fck[m > 0 ? 2 * ((m - 1) * nl + t) : 2 * t + 1];
+        const double bfP = f.x, bfM = f.y;
         // alpha registers hold one half of the mini-block: the second half's alphas from a
         // forward pass over all 16 positions, then (after its backward pass) the first half's
         // from a second forward pass — 32 fewer VGPRs than the whole mini-block's, for 2 extra
@@ -547,9 +548,12 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
                 const uint32_t d = code_at(cm, i);
                 const double2 ma = qa[(hi - 1 - i) % (EST_PFD + 1)],
                               mb = qb[(hi - 1 - i) % (EST_PFD + 1)];
-                if (t == 0 && m == 0 && i == 0) {   // gamma_0 = a_0 * y_0 / 2^47 -> init counts
-                    g0P = alP[0] * yP;
-                    g0M = alM[0] * yM;
+                if (t == 0 && m == 0 && i == 0) {   // gamma_0 = a_0 * y_0 / 2^47 -> init counts,
+                    // added at once (nothing stays live across the main loop for it)
+                    const uint32_t b0 = pk[0] & 3u;
+                    unsigned long long* ra = acc + 2 * kSlab * (c % kAccRep);
+                    acc128_add(ra + 2 * (64 + b0), to_fixed_scaled(alP[0] * yP), false);
+                    acc128_add(ra + 2 * (64 + b0 + 4), to_fixed_scaled(alM[0] * yM), false);
                     continue;
                 }
                 const double uP = i > lo ? alP[i - 1 - lo] : (lo > 0 ? hP : bfP);
@@ -604,35 +608,30 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
 #endif
     __syncthreads();
     CPG_EST_MARK(T6)
-    // chunk totals: row t = d * 4 + k, the sum of its 16 columns (integer: exact in any order)
-    if (t < 64) {
-        const unsigned long long* row = bins + bin_of(t >> 2, t & 3) * 16;
+    // the epilogue's indices from an opaque copy of the thread index: the compiler would
+    // otherwise keep the prologue's (shuffle) indices live across the main loop, in scratch
+    int te = threadIdx.x;
+    asm volatile("" : "+v"(te));
+    // chunk totals: row te = d * 4 + k, the sum of its 16 columns (integer: exact in any order)
+    if (te < 64) {
+        const unsigned long long* row = bins + bin_of(te >> 2, te & 3) * 16;
         unsigned long long s = 0;
 #pragma unroll
-        for (int col = 0; col < 16; ++col) s += row[(col + t) & 15];   // rotated: no conflicts
-        part[t] = s;
+        for (int col = 0; col < 16; ++col) s += row[(col + te) & 15];   // rotated: no conflicts
+        part[te] = s;
     }
     __syncthreads();
     CPG_EST_MARK(T7)
-    unsigned long long* racc = acc + 2 * kSlab * (c % kAccRep);
     // chunk results -> the global 128-bit accumulators: xi bins and the init posteriors in
     // 2^-47 units, the log-likelihood in signed 2^-24 units
-    if (t < 64) {   // row t = d * 4 + k (wave 0)
-        unsigned long long s = part[t];
+    if (te < 64) {   // row te = d * 4 + k (wave 0)
+        unsigned long long s = part[te];
         // the class's 4 raw sums (lanes 4d .. 4d+3) -> its position count -> K removed
         unsigned long long S = s;
         S += __shfl_xor(S, 1);
         S += __shfl_xor(S, 2);
         s -= class_count(S) * kMagicBits;
-        acc128_add(racc + 2 * t, s, false);
-    }
-    if (t == 0) {
-        acc128_add(racc + 2 * (64 + o0), to_fixed_scaled(g0P), false);   // already 2^47-scaled
-        acc128_add(racc + 2 * (64 + o0 + 4), to_fixed_scaled(g0M), false);
-    }
-    if (t == nl - 1) {
-        const long long L = llrint(ldexp(loglik, kLogFix));
-        acc128_add(racc + 2 * 72, (unsigned long long)L, L < 0);
+        acc128_add(racc + 2 * te, s, false);
     }
     // done != nullptr: the last workgroup to finish converts the sums (one launch per call)
     if (done && last_workgroup(done, reinterpret_cast<int*>(part))) {
