@@ -112,7 +112,19 @@ def cpu_baseline(seed, sample_bases, threads):
             "cpu": _cpu_model()}
 
 
-def cold_cache_steps(ln, dp, ds, N, model0, model1, nsteps, main_s, dev, flush_mb=1024):
+def train_step(ctx, model0, dp, ds, N, ecnt, lcnt, fused):
+    """The training pass: E-step (model0) + labelled counts of the same chunks — one launch
+    (cpg_train_pass_d) or the two single calls (--separate-train)."""
+    from cpgisland_amd import device as D
+    if fused:
+        D.train_pass(ctx, model0, dp, ds, N, TRAIN, estep_out=ecnt, counts_out=lcnt)
+    else:
+        D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
+        D.count_labelled(ctx, dp, ds, N, TRAIN, out=lcnt)
+
+
+def cold_cache_steps(ln, dp, ds, N, model0, model1, nsteps, main_s, dev, flush_mb=1024,
+                     fused=True):
     """The step on one stream, each behind a 1 GiB scratch write that evicts the shard from
     the 256 MB Infinity Cache; HIP events bracket the step's kernels only (not the flush)."""
     from cpgisland_amd import device as D
@@ -123,8 +135,7 @@ def cold_cache_steps(ln, dp, ds, N, model0, model1, nsteps, main_s, dev, flush_m
             buf.fill_(1.0)
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
-            D.bw_estep(ln["ctx"], model0, dp, N, TRAIN, out=ln["ecnt"])
-            D.count_labelled(ln["ctx"], dp, ds, N, TRAIN, out=ln["lcnt"])
+            train_step(ln["ctx"], model0, dp, ds, N, ln["ecnt"], ln["lcnt"], fused)
             D.viterbi(ln["ctx"], model1, dp, N, DECODE, sign_out=ln["so"], score=ln["score"])
             D.islands(ln["ctx"], dp, ln["so"], N, DECODE, cap=ln["iout"].shape[0],
                       out=ln["iout"], count=ln["icnt"])
@@ -156,6 +167,9 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--bases", type=int, default=N_PER_GPU, help="bases per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--separate-train", action="store_true",
+                    help="E-step and labelled counts as two launches instead of the fused "
+                         "training pass (cpg_train_pass_d)")
     ap.add_argument("--cpu-sample", type=int, default=192 * DECODE)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
@@ -267,6 +281,7 @@ def main():
     # point of record): 10 per step cost ~9 % of the overlapped throughput, 4 per step ~3 %,
     # the E-step's 2 per step plus the decode's on every 4th step ~1 %.
     full_ev = args.phase_events or args.serial
+    fused = not args.separate_train
     names = ("estep", "counts", "reduce", "viterbi", "islands") if full_ev else ("estep", "decode")
     # one pair of HIP events per phase per timed step, read after the final synchronize (no
     # host round trip between steps)
@@ -352,12 +367,18 @@ def main():
                 if pi == 0:
                     mark("islands", 1)
         with torch.cuda.stream(s_tr):
-            mark("estep", 0)
-            D.bw_estep(cx, model0, dp, N, TRAIN, out=ln["ecnt"])
-            mark("estep", 1)
-            mark("counts", 0)
-            D.count_labelled(cx, dp, ds, N, TRAIN, out=ln["lcnt"])
-            mark("counts", 1)
+            if fused:   # "estep" = the whole training pass (E-step + labelled counts)
+                mark("estep", 0)
+                D.train_pass(cx, model0, dp, ds, N, TRAIN, estep_out=ln["ecnt"],
+                             counts_out=ln["lcnt"])
+                mark("estep", 1)
+            else:
+                mark("estep", 0)
+                D.bw_estep(cx, model0, dp, N, TRAIN, out=ln["ecnt"])
+                mark("estep", 1)
+                mark("counts", 0)
+                D.count_labelled(cx, dp, ds, N, TRAIN, out=ln["lcnt"])
+                mark("counts", 1)
             mark("reduce", 0)
             if dist:   # the reducer: int64 sums are exact in any order; fp64 in rank order
                 cdist.merge_counts_i64(ln["lcnt"])
@@ -407,7 +428,8 @@ def main():
         elapsed = float(t.item())
     cold = None
     if args.cold_steps > 0 and not dist and not args.flush_mb:
-        cold = cold_cache_steps(lanes[0], dp, ds, N, model0, model1, args.cold_steps, main_s, dev)
+        cold = cold_cache_steps(lanes[0], dp, ds, N, model0, model1, args.cold_steps, main_s, dev,
+                                fused=fused)
     steps = args.steps
     ms_per_step = elapsed * 1e3 / steps
     value = N * world * steps / elapsed
@@ -421,13 +443,17 @@ def main():
         # dominant kernel (rocprof, profiles/): the E-step chunk kernel.  achieved = its
         # algorithmic bytes per launch / the phase's mean duration (HIP events on its stream;
         # the phase is k_estep_chunk + the ~4 us one-workgroup final kernel).
+        # (fused: the phase is the training pass, whose one kernel also reads the label bits)
         dom = "estep"
-        alg_bytes = BYTES_PER_BASE[dom] * N
+        bpb = BYTES_PER_BASE[dom] + (0.125 if fused else 0.0)
+        alg_bytes = bpb * N
         ach = alg_bytes / (phases[dom] / 1e3) / 1e9 if phases[dom] > 0 else 0.0
-        roof = {"bound": "hbm", "kernel": "k_estep_chunk", "phase": dom,
+        roof = {"bound": "hbm",
+                "kernel": ("k_estep_chunk<true> (training pass: E-step + labelled counts)"
+                           if fused else "k_estep_chunk"), "phase": dom,
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
-                "algorithmic_bytes": alg_bytes, "bytes_per_base": BYTES_PER_BASE[dom]}
+                "algorithmic_bytes": alg_bytes, "bytes_per_base": bpb}
         pmc = _pmc_traffic("k_estep_chunk", N)
         if pmc:
             roof["traffic"] = pmc["traffic_bytes"]
@@ -458,6 +484,8 @@ def main():
                "config": {"workload": "C2: 46 Mbp chr21-sized per GPU; BW E-step + labelled "
                                       "counts + RCCL reduce + exact Viterbi + islands",
                           "streams": 1 if args.serial else 2,
+                          "train_pass": ("fused: cpg_train_pass_d, E-step + labelled counts in "
+                                         "one launch" if fused else "separate launches"),
                           "decode_priority": "high" if (args.prio and not args.serial) else "normal",
                           "step_overlap": not (args.no_overlap or args.serial),
                           "pipeline_lanes": nlanes,

@@ -343,6 +343,38 @@ int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packe
     return CPG_OK;
 }
 
+int cpg_train_pass_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                     const uint32_t* d_sign, int64_t nbases, int64_t chunk_len,
+                     double* d_estep_counts, int64_t* d_label_counts, void* stream) {
+    if (!ctx || !model || !d_estep_counts || !d_label_counts)
+        return set_error(CPG_E_INVALID, "null argument");
+    int rc = check_layout(d_packed, nbases, chunk_len);
+    if (rc) return rc;
+    if (!aligned16(d_sign)) return set_error(CPG_E_INVALID, "sign buffer not 16-byte aligned");
+    if ((rc = model_check_deterministic(model))) return rc;
+    if (chunk_len % 4096 || chunk_len > 65536)
+        return set_error(CPG_E_INVALID, "E-step chunk_len must be a multiple of 4096, <= 65536");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    const int64_t nch = nbases / chunk_len;
+    void *wse, *wsc;
+    if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nch, chunk_len), &wse))) return rc;
+    if ((rc = ws_get(ctx, WS_COUNT, count_ws_bytes(nch), &wsc))) return rc;
+    const double2* gtab = nullptr;
+    if (nch > 0 && (rc = est_tables(ctx, model, &gtab))) return rc;
+    hipStream_t s = pick(ctx, stream);
+    if (train_fusable(chunk_len)) {
+        CPG_HIP(launch_train(*model, d_packed, d_sign, nch, chunk_len,
+                             (unsigned long long*)wse, d_estep_counts,
+                             (unsigned long long*)wsc, d_label_counts, s, gtab));
+    } else {
+        CPG_HIP(launch_estep(*model, d_packed, nch, chunk_len, (unsigned long long*)wse,
+                             d_estep_counts, s, PART_ALL, gtab));
+        CPG_HIP(launch_count(d_packed, d_sign, nch, chunk_len, (uint64_t*)wsc, d_label_counts, s));
+    }
+    return CPG_OK;
+}
+
 int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compat_quirks,
                  uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result,
                  void* stream) {

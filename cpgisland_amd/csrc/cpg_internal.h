@@ -183,6 +183,12 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
                         int64_t chunk_len, unsigned long long* acc, double* out,
                         hipStream_t s, int parts = PART_ALL, const double2* gtab = nullptr);
 size_t estep_ws_bytes(int64_t nchunks, int64_t chunk_len);
+// the fused training pass (E-step + labelled counts in one launch; k_estep.hip)
+bool train_fusable(int64_t chunk_len);
+hipError_t launch_train(const cpg_model& model, const uint32_t* packed, const uint32_t* sign,
+                        int64_t nchunks, int64_t chunk_len, unsigned long long* acc, double* out,
+                        unsigned long long* cacc, int64_t* cout, hipStream_t s,
+                        const double2* gtab);
 
 // ragged contig batches (k_contigs.hip)
 size_t contigs_sort_ws_bytes(int64_t n);

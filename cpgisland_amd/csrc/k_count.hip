@@ -2,11 +2,10 @@
 //
 // Training-side counterpart of the BW mapper stripes (init / transition / emission rows,
 // CpGIslandFinder.java:200) computed from hard labels: state s_t = base_t + (sign_t?0:4).
-// Streams 2-bit packed bases (16 B per lane = 64 bases) and sign bits (8 B per lane),
-// builds per-lane dinucleotide bitmasks and counts them with v_bcnt (popcount+add), so a
-// base costs a few VALU ops and no LDS traffic.  Sign classes ride a uniform fast path:
-// inside an island or background run every transition is ++ or --, and only lane-blocks
-// that straddle an island boundary take the general four-class path.
+// Streams 2-bit packed bases (16 B per lane = 64 bases) and sign bits (8 B per lane) in
+// grid-stride batches whose loads are all in flight before any block is counted, and counts
+// with v_bcnt over base bit-masks (count_dev.h; shared with the fused training pass in
+// k_estep.hip).
 //
 // Per-workgroup partial counts (and the init states of the chunks starting in the
 // workgroup) are added to 72 global 64-bit accumulators (integer atomics: exact and
@@ -15,51 +14,22 @@
 // identities) and re-zeroes the accumulators.  One launch per call (a separate one-workgroup
 // finalize launch for the streamed genome, which accumulates every window first).
 
-#include "cpg_internal.h"
+#include "count_dev.h"
 
 namespace cpg {
 namespace {
 
+using cnt::kRaw;
 constexpr int kCountThreads = 256;
-constexpr int kRaw = 72;        // tot[16] pp[16] pm[16] mp[16] init[8]
-// workgroups add into kCntRep replicated accumulator sets (blockIdx % kCntRep) so that the
-// workgroups do not serialise on 72 device-scope atomic addresses; the finalize sums them
-#ifndef CNT_REP
-#define CNT_REP 16
-#endif
+constexpr int kCntRep = cnt::kRep;
 #ifndef CNT_GRID
 #define CNT_GRID 512   // measured: 2048 / 1024 / 512 workgroups 19.0 / 14.6 / 12.9 us at 46 Mbp
 #endif
-constexpr int kCntRep = CNT_REP;
-constexpr uint32_t M55 = 0x55555555u;
-
-struct Masks {
-    uint32_t e[4];   // bit 2k set iff base k == b
-};
-
-__device__ __forceinline__ Masks base_masks(uint32_t w) {
-    uint32_t h = w >> 1;
-    Masks m;
-    m.e[0] = ~(w | h) & M55;
-    m.e[1] = w & ~h & M55;
-    m.e[2] = h & ~w & M55;
-    m.e[3] = w & h & M55;
-    return m;
-}
-
-// spread 16 bits (bit k) to even bit positions (bit 2k)
-__device__ __forceinline__ uint32_t spread16(uint32_t x) {
-    x &= 0xFFFFu;
-    x = (x | (x << 8)) & 0x00FF00FFu;
-    x = (x | (x << 4)) & 0x0F0F0F0Fu;
-    x = (x | (x << 2)) & 0x33333333u;
-    x = (x | (x << 1)) & 0x55555555u;
-    return x;
-}
-
-__device__ void final_counts(const uint64_t* raw, int t, int64_t* __restrict__ out);
-template <bool kAgent>
-__device__ void finalize(unsigned long long* gacc, uint64_t* raw, int64_t* out);
+#ifndef CNT_BATCH
+#define CNT_BATCH 6    // blocks per lane in flight (46 Mbp: 5.5 blocks per lane at 512 x 256)
+#endif
+constexpr int kBatch = CNT_BATCH;
+static_assert(kBatch <= cnt::Lane::kMaxBlocks, "16-bit wave sums");
 
 // done != nullptr: the last workgroup to finish also finalizes (one launch per call)
 __global__ __launch_bounds__(kCountThreads) void k_count_main(
@@ -67,190 +37,105 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
     const uint32_t* __restrict__ packed, const uint32_t* __restrict__ sign, int64_t nblk,
     int64_t blk_per_chunk, unsigned long long* __restrict__ gacc, unsigned int* done,
     int64_t* __restrict__ out) {
-    uint32_t tot[16], pp[16], pm[16], mp[16];
-#pragma unroll
-    for (int d = 0; d < 16; ++d) tot[d] = pp[d] = pm[d] = mp[d] = 0u;
-    __shared__ uint32_t sinit[8];   // states of the chunks' first bases (rare: LDS atomics)
-    if (threadIdx.x < 8) sinit[threadIdx.x] = 0u;
+    __shared__ uint32_t scnt[kRaw];   // the workgroup's counters (LDS atomics)
+    __shared__ uint64_t raw[kRaw];
+    __shared__ int s_last;
+    const int t = threadIdx.x;
+    const bool pow2 = (blk_per_chunk & (blk_per_chunk - 1)) == 0;
+#ifdef CNT_STAMP
+    const unsigned long long T0 = wall_clock64();
+    unsigned long long T1 = 0, T2 = 0;
+#endif
+    if (t < kRaw) scnt[t] = 0u;
     __syncthreads();
-
+    cnt::Lane lc;
     const int64_t stride = (int64_t)gridDim.x * blockDim.x;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < nblk; i += stride) {
-        const uint4 w = packed4[i];
-        const uint2 s = sign2[i];
-        const bool cstart = (i % blk_per_chunk) == 0;
-        uint32_t wprev = 0, sprev = 0;
-        if (cstart) atomicAdd(&sinit[(w.x & 3u) + ((s.x & 1u) ? 0u : 4u)], 1u);
-        if (!cstart) {
-            wprev = packed[4 * i - 1];
-            sprev = sign[2 * i - 1] >> 31;
-        }
-        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-        Masks cur[4], prv[4];
+    // grid-stride batches: all of a batch's words are loaded before any is counted, so a lane
+    // waits for memory once per batch (the loop is latency-bound, not VALU-bound)
+    // (the loop bound is the workgroup's first block: every lane runs every batch, so the
+    // flush's shuffles see the whole wave)
+    for (int64_t g0 = (int64_t)blockIdx.x * blockDim.x; g0 < nblk; g0 += kBatch * stride) {
+        const int64_t i0 = g0 + t;
+        uint4 w[kBatch];
+        uint2 s[kBatch];
+        uint32_t wp[kBatch], sp[kBatch];
+        // unconditional loads (index clamped) and no arithmetic on their results here: a
+        // load under a branch, or a shift of a loaded word, makes the compiler wait for it
+        // before issuing the next — one memory round trip per block instead of per batch
 #pragma unroll
-        for (int k = 0; k < 4; ++k) cur[k] = base_masks(ww[k]);
+        for (int r = 0; r < kBatch; ++r) {
+            const int64_t i = min(i0 + r * stride, nblk - 1);
+            const int64_t ip = i > 0 ? i - 1 : 0;
+            w[r] = packed4[i];
+            s[r] = sign2[i];
+            wp[r] = packed[4 * ip + 3];
+            sp[r] = sign[2 * ip + 1];
+        }
+#ifdef CNT_STAMP
         {
-            uint32_t wp = __builtin_amdgcn_alignbit(ww[0], wprev, 30);
-            prv[0] = base_masks(wp);
+            uint32_t x = 0;
+#pragma unroll
+            for (int r = 0; r < kBatch; ++r) x += w[r].x + s[r].y + wp[r] + sp[r];
+            if (x == 0x9999999u) scnt[0] = x;
+            T1 = wall_clock64();
         }
+#endif
 #pragma unroll
-        for (int k = 1; k < 4; ++k)
-#pragma unroll
-            for (int b = 0; b < 4; ++b)
-                prv[k].e[b] = __builtin_amdgcn_alignbit(cur[k].e[b], cur[k - 1].e[b], 30);
-        if (cstart) {
-#pragma unroll
-            for (int b = 0; b < 4; ++b) prv[0].e[b] &= ~1u;   // no transition into pos 0
-        }
-        const bool all_minus = (s.x == 0u) && (s.y == 0u) && (cstart || sprev == 0u);
-        const bool all_plus = (s.x == ~0u) && (s.y == ~0u) && (cstart || sprev == 1u);
-#pragma unroll
-        for (int k = 0; k < 4; ++k)
-#pragma unroll
-            for (int p = 0; p < 4; ++p)
-#pragma unroll
-                for (int b = 0; b < 4; ++b)
-                    tot[p * 4 + b] += __popc(prv[k].e[p] & cur[k].e[b]);
-        if (!all_minus) {
-            if (all_plus) {
-#pragma unroll
-                for (int k = 0; k < 4; ++k)
-#pragma unroll
-                    for (int p = 0; p < 4; ++p)
-#pragma unroll
-                        for (int b = 0; b < 4; ++b)
-                            pp[p * 4 + b] += __popc(prv[k].e[p] & cur[k].e[b]);
-            } else {
-                // general path: per word spread sign masks
-                const uint32_t sw[4] = {s.x & 0xFFFFu, s.x >> 16, s.y & 0xFFFFu, s.y >> 16};
-                uint32_t sprv = sprev;
-#pragma unroll
-                for (int k = 0; k < 4; ++k) {
-                    uint32_t S = spread16(sw[k]);
-                    uint32_t Sp = (S << 2) | (sprv & 1u);
-                    sprv = sw[k] >> 15;
-                    uint32_t SS = Sp & S, SN = Sp & ~S, NS = ~Sp & S;
-#pragma unroll
-                    for (int p = 0; p < 4; ++p)
-#pragma unroll
-                        for (int b = 0; b < 4; ++b) {
-                            uint32_t D = prv[k].e[p] & cur[k].e[b];
-                            pp[p * 4 + b] += __popc(D & SS);
-                            pm[p * 4 + b] += __popc(D & SN);
-                            mp[p * 4 + b] += __popc(D & NS);
-                        }
-                }
+        for (int r = 0; r < kBatch; ++r) {
+            const int64_t i = i0 + r * stride;
+            if (i < nblk) {
+                // (a power-of-two chunk — the reference's 0x10000 — needs no 64-bit modulo)
+                const bool cstart = pow2 ? (i & (blk_per_chunk - 1)) == 0 : (i % blk_per_chunk) == 0;
+                if (cstart) atomicAdd(&scnt[64 + cnt::init_state(w[r].x, s[r].x)], 1u);
+                lc.block(w[r], s[r], wp[r], sp[r] >> 31, cstart, scnt);
             }
         }
-    }
-
-    // wave reduction by recursive halving: after 6 levels lane L holds the wave sum of
-    // counter L (63 shuffles instead of 64 x 6)
-    uint32_t v[64];
-#pragma unroll
-    for (int d = 0; d < 16; ++d) {
-        v[d] = tot[d];
-        v[16 + d] = pp[d];
-        v[32 + d] = pm[d];
-        v[48 + d] = mp[d];
-    }
-    const int lane = threadIdx.x & 63;
-#pragma unroll
-    for (int lvl = 0; lvl < 6; ++lvl) {
-        const int o = 32 >> lvl;
-        const bool up = (lane & o) != 0;
-#pragma unroll
-        for (int i = 0; i < o; ++i) {
-            uint32_t send = up ? v[i] : v[i + o];
-            uint32_t keep = up ? v[i + o] : v[i];
-            v[i] = keep + (uint32_t)__shfl_xor((int)send, o);
-        }
-    }
-    __shared__ uint32_t wsum[kCountThreads / 64][64];
-    wsum[threadIdx.x >> 6][lane] = v[0];
-    __syncthreads();
-    if (threadIdx.x < kRaw) {
-        uint64_t acc = 0;
-        if (threadIdx.x < 64) {
-#pragma unroll
-            for (int w = 0; w < kCountThreads / 64; ++w) acc += wsum[w][threadIdx.x];
-        } else {
-            acc = sinit[threadIdx.x - 64];
-        }
-#ifdef CNT_NOATOM   // measurement only: wrong counts
-        if (acc == 0x123456789ull)
-#else
-        if (acc)
+#ifdef CNT_STAMP
+        T2 = wall_clock64();
 #endif
-            atomicAdd(gacc + (blockIdx.x % kCntRep) * kRaw + threadIdx.x,
-                           (unsigned long long)acc);
+        lc.flush(scnt);   // per batch: kBatch <= Lane::kMaxBlocks
     }
-    __shared__ int s_last;
-    __shared__ uint64_t raw[kRaw];
+    __syncthreads();
+#ifdef CNT_STAMP
+    const unsigned long long T3 = wall_clock64();
+#endif
+    if (t < kRaw) {
+        const uint32_t v = cnt::raw_of(scnt, t);
+#ifdef CNT_NOATOM   // measurement only: wrong counts
+        if (v == 0x12345678u)
+#else
+        if (v)
+#endif
+            atomicAdd(gacc + (blockIdx.x % kCntRep) * kRaw + t, (unsigned long long)v);
+    }
+#ifdef CNT_STAMP
+    __builtin_amdgcn_s_waitcnt(0);
+    __syncthreads();
+    const unsigned long long T4 = wall_clock64();
+    if (t == 0 && (blockIdx.x % 64 == 0 || blockIdx.x == gridDim.x - 1))
+        printf("cnt wg %d: start %llu loads %llu count %llu flush+bar %llu atomics %llu\n",
+               blockIdx.x, T0 % 1000000, T1 - T0, T2 - T1, T3 - T2, T4 - T3);
+#endif
+#ifdef CNT_NOFIN   // measurement only: no finalize
+    if (done && blockIdx.x == 0x7fffffff) {
+#else
     if (done && last_workgroup(done, &s_last)) {
-        finalize<true>(gacc, raw, out);
+#endif
+        if (t < kRaw) cnt::fin_load<true>(gacc, raw, t);
+        __syncthreads();
+        cnt::fin_store(gacc, raw, out, t, blockDim.x);
         reset_done(done);
     }
 }
 
-// the cpg_counts_i64 assembly from the 72 accumulators (replicas summed), which it re-zeroes;
-// kAgent: the accumulators were written by workgroups of the same launch
-template <bool kAgent>
-__device__ void finalize(unsigned long long* gacc, uint64_t* raw, int64_t* out) {
-    const int t = threadIdx.x;
-    if (t < kRaw) {
-        uint64_t v = 0;
-        for (int r = 0; r < kCntRep; ++r)
-            v += kAgent ? load_agent(gacc + r * kRaw + t) : gacc[r * kRaw + t];
-        raw[t] = v;
-    }
-    __syncthreads();
-    for (int i = t; i < kRaw * kCntRep; i += blockDim.x) gacc[i] = 0ull;
-    for (int i = t; i < 124; i += blockDim.x) final_counts(raw, i, out);
-}
-
-// One workgroup: the cpg_counts_i64 assembly from the 72 accumulators, which it re-zeroes.
+// One workgroup: the cpg_counts_i64 assembly from accumulators filled by earlier launches
+// (the streamed genome), which it re-zeroes.
 __global__ __launch_bounds__(128) void k_count_final(unsigned long long* __restrict__ gacc,
                                                      int64_t* __restrict__ out) {
     __shared__ uint64_t raw[kRaw];
-    finalize<false>(gacc, raw, out);
-}
-
-// cpg_counts_i64 from the 72 raw sums (tot | pp | pm | mp | init); thread t < 124
-__device__ void final_counts(const uint64_t* raw, int t, int64_t* __restrict__ out) {
-    // cpg_counts_i64 layout: init[8] trans[8][8] emit[8][4] dinuc[4][4] mono[4]; one
-    // output word per thread
-    int64_t v = 0;
-    if (t < 8) {
-        v = (int64_t)raw[64 + t];
-    } else if (t < 72) {
-        const int i = (t - 8) >> 3, j = (t - 8) & 7;      // trans[i][j]
-        const int d = (i & 3) * 4 + (j & 3), si = i >> 2, sj = j >> 2;
-        const int64_t tt = (int64_t)raw[d], ppv = (int64_t)raw[16 + d],
-                      pmv = (int64_t)raw[32 + d], mpv = (int64_t)raw[48 + d];
-        v = si == 0 ? (sj == 0 ? ppv : pmv) : (sj == 0 ? mpv : tt - ppv - pmv - mpv);
-    } else if (t < 104) {
-        const int s = (t - 72) >> 2, k = (t - 72) & 3;     // emit[s][k]
-        if (k == (s & 3)) {
-            v = (int64_t)raw[64 + s];
-            for (int r = 0; r < 8; ++r) {
-                const int d = (r & 3) * 4 + (s & 3), si = r >> 2, sj = s >> 2;
-                const int64_t tt = (int64_t)raw[d], ppv = (int64_t)raw[16 + d],
-                              pmv = (int64_t)raw[32 + d], mpv = (int64_t)raw[48 + d];
-                v += si == 0 ? (sj == 0 ? ppv : pmv) : (sj == 0 ? mpv : tt - ppv - pmv - mpv);
-            }
-        }
-    } else if (t < 120) {
-        const int p = (t - 104) >> 2, b = (t - 104) & 3;    // dinuc[p][b]
-        v = (int64_t)raw[p * 4 + b];
-    } else {
-        const int b = t - 120;                               // mono[b] = sum_p dinuc + inits
-        // every base at a chunk position > 0 is the cur base of one transition; position 0
-        // is counted by init
-        for (int p = 0; p < 4; ++p) v += (int64_t)raw[p * 4 + b];
-        v += (int64_t)raw[64 + b] + (int64_t)raw[64 + b + 4];
-    }
-    out[t] = v;
+    if (threadIdx.x < kRaw) cnt::fin_load<false>(gacc, raw, threadIdx.x);
+    __syncthreads();
+    cnt::fin_store(gacc, raw, out, threadIdx.x, blockDim.x);
 }
 
 }  // namespace

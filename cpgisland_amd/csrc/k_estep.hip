@@ -26,7 +26,7 @@
 #include <algorithm>
 #include <cmath>
 
-#include "cpg_internal.h"
+#include "count_dev.h"
 
 // The E-step is a tolerance-bound fp64 computation (unlike the bit-exact Viterbi): products
 // and sums may be contracted to FMAs here (the fixed-point conversion of a posterior becomes
@@ -253,6 +253,16 @@ __device__ __forceinline__ Codes lane_codes(const uint32_t* __restrict__ pk, int
     return c;
 }
 
+// __shfl_xor(v, m) with the lane address taken from an opaque thread index te (the builtin
+// derives it from the lane id, which the compiler then shares with the prologue's shuffles
+// and keeps live across the main loop)
+__device__ __forceinline__ unsigned long long xor_te(unsigned long long v, int te, int m) {
+    const int a = ((te & 63) ^ m) << 2;
+    const uint32_t lo = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)v);
+    const uint32_t hi = (uint32_t)__builtin_amdgcn_ds_bpermute(a, (int)(uint32_t)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 template <bool kAgent>
 __device__ void finalize(unsigned long long* acc, double* vsum, double* out);
 __device__ void final_estep(const double* v, int t, double* __restrict__ out);
@@ -270,10 +280,16 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 #ifndef CPG_EST_WPE
 #define CPG_EST_WPE 5
 #endif
+// kCnt: the fused training pass — each lane also counts its 64 bases' labelled transitions
+// (count_dev.h; sign = the label bits), added into the count accumulators cacc, and the last
+// workgroup finalizes both (cout: cpg_counts_i64).  Needs >= 256 lanes (chunks >= 16 Ki).
+template <bool kCnt>
 __global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(CPG_EST_WPE)))
 void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
                    unsigned long long* __restrict__ acc, const double2* __restrict__ gtab,
-                   unsigned int* done, double* __restrict__ out) {
+                   unsigned int* done, double* __restrict__ out,
+                   const uint32_t* __restrict__ sign, unsigned long long* __restrict__ cacc,
+                   int64_t* __restrict__ cout) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves
@@ -298,7 +314,31 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     // rather than per-lane reads of the kernel-argument model
     if (t < 32) TA[t] = gtab[t];   // TB = TA + 16
     const Codes cd0 = lane_codes(pk, t);   // (in flight across the barrier)
+    // fused counts: the workgroup's 72 count sums (LDS atomics) and the finalize's raw sums
+    // in the epilogue scratch `part` (free until the epilogue's first 76 words)
+    uint32_t* scnt = reinterpret_cast<uint32_t*>(part + 128);
+    uint2 sg = make_uint2(0u, 0u);
+    uint32_t sgp = 0u;
+    if (kCnt) {
+        if (t < cnt::kRaw) scnt[t] = 0u;
+        const uint32_t* sk = sign + c * (C / 32);
+        sg = *reinterpret_cast<const uint2*>(sk + 2 * t);
+        sgp = sk[t > 0 ? 2 * t - 1 : 0];   // (unconditional; its sign bit taken at use)
+    }
     __syncthreads();
+    if (kCnt) {   // the lane's 64 bases = one count block (its first is the chunk's first)
+        __builtin_amdgcn_sched_barrier(0);   // kept apart from phase 1: registers
+        if (t == 0) atomicAdd(&scnt[64 + cnt::init_state(cd0.raw[0], sg.x)], 1u);
+#ifndef CPG_FUSE_NOCOUNT   // measurement only: the sign loads without the counting
+        cnt::Lane lc;
+        lc.block(make_uint4(cd0.raw[0], cd0.raw[1], cd0.raw[2], cd0.raw[3]), sg, cd0.prev,
+                 sgp >> 31, t == 0, scnt);
+        lc.flush(scnt);
+#else
+        if (sg.x == 0x12345u && sgp == 7u) scnt[3] = 1u;
+#endif
+        __builtin_amdgcn_sched_barrier(0);
+    }
     // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4), from the rows
     for (int i = t; i < 1024; i += nl) {
         double x00 = 1.0, x01 = 0.0, x10 = 0.0, x11 = 1.0;
@@ -628,14 +668,22 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         unsigned long long s = part[te];
         // the class's 4 raw sums (lanes 4d .. 4d+3) -> its position count -> K removed
         unsigned long long S = s;
-        S += __shfl_xor(S, 1);
-        S += __shfl_xor(S, 2);
+        S += xor_te(S, te, 1);   // (lane addresses from te, see above)
+        S += xor_te(S, te, 2);
         s -= class_count(S) * kMagicBits;
         acc128_add(racc + 2 * te, s, false);
     }
+    if (kCnt && te >= 64 && te < 64 + cnt::kRaw) {   // waves 1-2: the count sums
+        const uint32_t v = cnt::raw_of(scnt, te - 64);
+        if (v) atomicAdd(cacc + (c % cnt::kRep) * cnt::kRaw + (te - 64), (unsigned long long)v);
+    }
     // done != nullptr: the last workgroup to finish converts the sums (one launch per call)
     if (done && last_workgroup(done, reinterpret_cast<int*>(part))) {
+        // the count replicas are read by waves 2-3 beside the E-step's (finalize's barrier)
+        uint64_t* craw = reinterpret_cast<uint64_t*>(part + 192);
+        if (kCnt && te >= 128 && te < 128 + cnt::kRaw) cnt::fin_load<true>(cacc, craw, te - 128);
         finalize<true>(acc, reinterpret_cast<double*>(part + 2), out);
+        if (kCnt) cnt::fin_store(cacc, craw, cout, te, nl);
         reset_done(done);
     }
 #ifdef CPG_DEBUG_ESTEP
@@ -713,6 +761,13 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
 // accumulators | done counter (in the 1 KiB tail)
 size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep + 1024; }
 
+namespace {
+size_t estep_lds(int lanes) {   // the union is sized for 16 waves; fewer lanes use a prefix
+    return kUnionOff + kUnionBytes + 16 * 64 * sizeof(unsigned long long) +
+           (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
+}
+}  // namespace
+
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t C, unsigned long long* acc, double* out, hipStream_t s,
                         int parts, const double2* gtab) {
@@ -721,18 +776,35 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
         return hipMemsetAsync(out, 0, 105 * sizeof(double), s);
     if ((parts & PART_ACC) && nchunks > 0) {
         const int lanes = (int)(C / kLanePos);
-        const size_t uni = kUnionBytes;   // sized for 16 waves; fewer lanes use a prefix
-        const size_t lds = kUnionOff + uni + 16 * 64 * sizeof(unsigned long long) +
-                           (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
         if (!gtab) return hipErrorInvalidValue;   // est_tables
         unsigned int* done =
             parts == PART_ALL ? reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep) : nullptr;
-        hipLaunchKernelGGL(k_estep_chunk, dim3((unsigned)nchunks), dim3(lanes), lds, s, model,
-                           packed, C, acc, gtab, done, out);
+        hipLaunchKernelGGL(k_estep_chunk<false>, dim3((unsigned)nchunks), dim3(lanes),
+                           estep_lds(lanes), s, model, packed, C, acc, gtab, done, out, nullptr,
+                           nullptr, nullptr);
         if (done) return hipGetLastError();
     }
     if (parts & PART_FINAL)
         hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);
+    return hipGetLastError();
+}
+
+bool train_fusable(int64_t C) { return C % 4096 == 0 && C >= 16384 && C <= (int64_t)kET * kLanePos; }
+
+hipError_t launch_train(const cpg_model& model, const uint32_t* packed, const uint32_t* sign,
+                        int64_t nchunks, int64_t C, unsigned long long* acc, double* out,
+                        unsigned long long* cacc, int64_t* cout, hipStream_t s,
+                        const double2* gtab) {
+    if (!train_fusable(C) || !gtab) return hipErrorInvalidValue;
+    if (nchunks == 0) {
+        hipError_t e = hipMemsetAsync(out, 0, 105 * sizeof(double), s);
+        return e != hipSuccess ? e : hipMemsetAsync(cout, 0, 124 * sizeof(int64_t), s);
+    }
+    const int lanes = (int)(C / kLanePos);
+    unsigned int* done = reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep);
+    hipLaunchKernelGGL(k_estep_chunk<true>, dim3((unsigned)nchunks), dim3(lanes),
+                       estep_lds(lanes), s, model, packed, C, acc, gtab, done, out, sign, cacc,
+                       cout);
     return hipGetLastError();
 }
 

@@ -82,6 +82,21 @@ def bw_estep(ctx: Context, model: HmmModel, packed: torch.Tensor, nbases: int,
     return out
 
 
+def train_pass(ctx: Context, model: HmmModel, packed: torch.Tensor, sign: torch.Tensor,
+               nbases: int, chunk_len: int = _lib.TRAIN_CHUNK,
+               estep_out: torch.Tensor | None = None, counts_out: torch.Tensor | None = None):
+    """bw_estep + count_labelled over the same chunks in one call (cpg_train_pass_d: one
+    launch for chunk_len >= 16384).  Returns (E-step counts f64, labelled counts i64)."""
+    if estep_out is None:
+        estep_out = torch.empty(_lib.COUNTS_F64_N, dtype=torch.float64, device=packed.device)
+    if counts_out is None:
+        counts_out = torch.empty(_lib.COUNTS_I64_N, dtype=torch.int64, device=packed.device)
+    m = model.to_struct()
+    check(lib.cpg_train_pass_d(ctx.handle, ptr(m), _dp(packed), _dp(sign), nbases, chunk_len,
+                               _dp(estep_out), _dp(counts_out), _stream()))
+    return estep_out, counts_out
+
+
 def viterbi(ctx: Context, model: HmmModel, packed: torch.Tensor, nbases: int,
             chunk_len: int = _lib.DECODE_CHUNK, sign_out: torch.Tensor | None = None,
             score: torch.Tensor | None = None):

@@ -179,6 +179,16 @@ int cpg_count_labelled_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t*
 int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                    int64_t nbases, int64_t chunk_len, double* d_counts, void* stream);
 
+/* The training pass in one call: cpg_bw_estep_d (model, d_packed -> d_estep_counts) and
+ * cpg_count_labelled_d (d_packed, d_sign -> d_label_counts) over the same whole chunk_len
+ * chunks (the mapper pass of :200 over the chunks of :130-141, with the labelled counts of
+ * the same chunks).  Results identical to the two calls; with chunk_len >= 16384 both run
+ * in ONE launch (each E-step lane also counts its 64 bases; one finalize), otherwise as
+ * the two launches.  chunk_len: a multiple of 4096, at most 65536. */
+int cpg_train_pass_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                     const uint32_t* d_sign, int64_t nbases, int64_t chunk_len,
+                     double* d_estep_counts, int64_t* d_label_counts, void* stream);
+
 /* Viterbi decode, HmmEvaluator.decode(trainedModel, chunk, true) (:260), of every
  * whole chunk_len chunk (tail not decoded, :256).  Output: the state path as sign bits
  * (state = base + (sign ? 0 : 4)), identical to Mahout's sequential fp64 Viterbi, and

@@ -241,22 +241,93 @@ def test_decode_errors(gpu_ctx):
 
 
 # ---------------------------------------------------------------- labelled counts
+def _labelled(kind, N, seed):
+    """(bases, signs) of a labelled-count case; "alternating" and "runs" put a sign change
+    at every / many positions (the counters' one-by-one border path, count_dev.h)."""
+    from cpgisland_amd import device as D
+    rng = np.random.default_rng(seed)
+    if kind == "synth":
+        packed, sign = D.synth_host(77 + seed, 0, N)
+        return pr.unpack(packed, N), pr.unpack_bits(sign, N)
+    obs = rng.integers(0, 4, N).astype(np.uint8)
+    if kind == "runs":
+        sg = np.repeat(np.arange(N) % 2, rng.integers(1, 9, N))[:N]
+    else:
+        sg = {"random": (rng.random(N) < 0.5), "plus": np.ones(N), "minus": np.zeros(N),
+              "alternating": np.arange(N) % 2}[kind]
+    return obs, sg.astype(np.uint8)
+
+
 @pytest.mark.parametrize("C", [256, 4096, 65536])
-@pytest.mark.parametrize("kind", ["random", "synth", "plus", "minus"])
+@pytest.mark.parametrize("kind", ["random", "synth", "plus", "minus", "alternating", "runs"])
 def test_counts_bit_exact(gpu_ctx, torch_dev, C, kind):
     from cpgisland_amd import device as D
-    rng = np.random.default_rng(C)
     N = 37 * C + 123
-    if kind == "synth":
-        packed, sign = D.synth_host(77, 0, N)
-        obs, sg = pr.unpack(packed, N), pr.unpack_bits(sign, N)
-    else:
-        obs = rng.integers(0, 4, N).astype(np.uint8)
-        sg = {"random": (rng.random(N) < 0.5), "plus": np.ones(N),
-              "minus": np.zeros(N)}[kind].astype(np.uint8)
+    obs, sg = _labelled(kind, N, C)
     dp, ds = _dev_genome(pr.pack(obs), pr.pack_bits(sg), torch_dev)
     got = D.count_labelled(gpu_ctx, dp, ds, N, C).cpu().numpy()
     assert np.array_equal(got, co.count_labelled(obs, sg, C))
+
+
+@pytest.mark.parametrize("kind", ["synth", "plus"])
+def test_counts_many_batches_vs_oracle(gpu_ctx, torch_dev, kind):
+    """160 Mbp: ~19 blocks per lane of the count grid, several batches and flushes per lane;
+    all-A / all-'+' puts 63 transitions of one class in every block (the 16-bit fields of a
+    wave sum would overflow without the per-batch flush)."""
+    from cpgisland_amd import device as D
+    N = 160_000_000 + 4321
+    if kind == "synth":
+        packed, sign = D.synth_host(8, 0, N)
+        obs, sg = pr.unpack(packed, N), pr.unpack_bits(sign, N)
+    else:
+        obs, sg = np.zeros(N, np.uint8), np.ones(N, np.uint8)
+        packed, sign = pr.pack(obs), pr.pack_bits(sg)
+    dp, ds = _dev_genome(packed, sign, torch_dev)
+    got = D.count_labelled(gpu_ctx, dp, ds, N, TRAIN).cpu().numpy()
+    assert np.array_equal(got, co.count_labelled(obs, sg, TRAIN))
+
+
+@pytest.mark.parametrize("C", [4096, 16384, 65536])
+@pytest.mark.parametrize("kind", ["synth", "random", "alternating"])
+def test_train_pass_equals_separate_calls(gpu_ctx, torch_dev, C, kind):
+    """cpg_train_pass_d (one launch for C >= 16 Ki: each E-step lane also counts its 64
+    bases) == cpg_bw_estep_d + cpg_count_labelled_d: E-step bitwise, counts bit-exact vs
+    the oracle."""
+    from cpgisland_amd import device as D
+    N = 11 * C + 321
+    obs, sg = _labelled(kind, N, C + 1)
+    dp, ds = _dev_genome(pr.pack(obs), pr.pack_bits(sg), torch_dev)
+    m = co.initial_model()
+    e, c = D.train_pass(gpu_ctx, _model(m), dp, ds, N, C)
+    e, c = e.cpu().numpy(), c.cpu().numpy()
+    assert np.array_equal(c, co.count_labelled(obs, sg, C))
+    assert np.array_equal(e, D.bw_estep(gpu_ctx, _model(m), dp, N, C).cpu().numpy())
+    ref = co.estep(m, obs, C)
+    nz = ref != 0
+    assert np.max(np.abs(e[nz] - ref[nz]) / np.abs(ref[nz])) < ESTEP_RTOL
+
+
+def test_train_pass_interleaved_with_single_calls(gpu_ctx, torch_dev):
+    """The fused pass shares the count / E-step accumulators and the E-step's done counters
+    with the single calls: any interleaving and grid size leaves them re-zeroed."""
+    from cpgisland_amd import device as D
+    m = co.initial_model()
+    packed, sign = D.synth_host(321, 0, 41 * TRAIN)
+    obs, truth = pr.unpack(packed, 41 * TRAIN), pr.unpack_bits(sign, 41 * TRAIN)
+    dp, ds = _dev_genome(packed, sign, torch_dev)
+    for i, nch in enumerate([2, 41, 1, 17, 41, 3]):
+        n = nch * TRAIN + 50
+        cref = co.count_labelled(obs[:n], truth[:n], TRAIN)
+        eref = co.estep(m, obs[:n], TRAIN)
+        nz = eref != 0
+        e, c = D.train_pass(gpu_ctx, _model(m), dp, ds, n, TRAIN)
+        assert np.array_equal(c.cpu().numpy(), cref), nch
+        e = e.cpu().numpy()
+        assert np.max(np.abs(e[nz] - eref[nz]) / np.abs(eref[nz])) < ESTEP_RTOL, nch
+        if i % 2:
+            assert np.array_equal(D.count_labelled(gpu_ctx, dp, ds, n, TRAIN).cpu().numpy(), cref)
+        else:
+            assert np.array_equal(D.bw_estep(gpu_ctx, _model(m), dp, n, TRAIN).cpu().numpy(), e)
 
 
 def test_counts_full_size_properties(gpu_ctx, torch_dev):

@@ -1,5 +1,5 @@
 """Median time (HIP events) of one hot-path phase on 46 Mbp for the libcpg build named by
-CPG_LIB_OVERRIDE (dev tool).  PHASE = estep | counts | viterbi | islands."""
+CPG_LIB_OVERRIDE (dev tool).  PHASE = estep | counts | train | viterbi | islands."""
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -21,6 +21,7 @@ icnt = torch.zeros(1, dtype=torch.int64, device=dev)
 D.viterbi(ctx, m, dp, N, 1 << 20, sign_out=so)
 ph = {"estep": lambda: D.bw_estep(ctx, m, dp, N, 65536, out=ec),
       "counts": lambda: D.count_labelled(ctx, dp, ds, N, 65536, out=lc),
+      "train": lambda: D.train_pass(ctx, m, dp, ds, N, 65536, estep_out=ec, counts_out=lc),
       "viterbi": lambda: D.viterbi(ctx, m, dp, N, 1 << 20, sign_out=so),
       "islands": lambda: D.islands(ctx, dp, so, N, 1 << 20, cap=1 << 20, out=iout, count=icnt)}
 name = os.path.basename(os.environ.get("CPG_LIB_OVERRIDE", "") or "default")
