@@ -525,6 +525,22 @@ __device__ void vit_irregular(const VitConsts& vc, const uint32_t* packed, const
                               double4* __restrict__ comp3, int64_t c, const double2* sA,
                               const double2* sB);
 
+// Segment path (chunks of a multiple of 256 blocks, e.g. 1 Mi): each regular workgroup (256
+// blocks of one chunk = one "segment") also runs a segmented scan of its exact composites,
+// barriers (every non-REGULAR block) resetting it, and writes per block rx = the product of
+// the REGULAR composites between the last barrier before it in the segment (or the segment
+// start) and the block, plus a SegSum (barrier mask, lead = product before the first barrier,
+// tail = product after the last).  K4 then touches only the barriers and 16 summaries per
+// chunk, and K5 derives every block's entry from rx and its anchor (the last barrier before
+// it, or the segment's entry): no per-chunk pass over every block's records.
+struct SegSum {
+    double4 lead, tail;
+    unsigned long long mask[4];   // bit l: block (segment start + l) is a barrier
+};
+__device__ __forceinline__ C64 shfl_up_c64(const C64& x, int d) {
+    return {__shfl_up(x.pp, d), __shfl_up(x.pm, d), __shfl_up(x.mp, d), __shfl_up(x.mm, d)};
+}
+
 __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitTables* vt,
                                                         const uint32_t* packed, Geo g,
                                                         VitPlan* __restrict__ plan,
@@ -532,7 +548,9 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
                                                         uint32_t* status, unsigned main_grid,
                                                         const longlong2* __restrict__ aent,
                                                         const int32_t* __restrict__ irrlist,
-                                                        const int32_t* __restrict__ irrcount) {
+                                                        const int32_t* __restrict__ irrcount,
+                                                        double4* __restrict__ rx,
+                                                        SegSum* __restrict__ seg) {
     // per binade slot: single-step halves sA/sB [16] (one 256-B bank row each) and 2-step
     // composites over 3-base windows, halves P2A = (pp, pm), P2B = (mp, mm) [64].  Every
     // entry is a sum of binade-rounded constants: exact on the binade's grid.
@@ -606,11 +624,12 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
         }
     }
     __syncthreads();
-    if (!reg) return;
+    if (!reg && !seg) return;   // (segment path: every lane takes part in the scan below)
     const uint32_t* pk = chunk_ptr(packed, g, c);
     const int slot = p.e_pre - vc.emin;
     C64 acc = c64_id();
-    if (g.full(k) && four) {
+    if (!reg) {
+    } else if (g.full(k) && four) {
         const BlockWords bw = load_block(pk, k);
         pipelined<4, 64>(
             [&](int j) {   // 5-base window of steps 4j .. 4j+3
@@ -642,11 +661,54 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
             c64_step(acc, a.x, a.y, b.x, b.y);
         });
     }
-    if (!c64_exact(acc, p.e_pre, vc.spread)) {
-        plan[gid].type = PLAN_SEQ;   // exactness not guaranteed: let K4 run it sequentially
+    const bool exact = reg && c64_exact(acc, p.e_pre, vc.spread);
+    // exactness not guaranteed: K4 runs the block sequentially
+    if (reg && !exact) plan[gid].type = PLAN_SEQ;
+    if (!seg) {
+        if (exact) comp3[gid] = make_double4(acc.pp, acc.pm, acc.mp, acc.mm);
         return;
     }
-    comp3[gid] = make_double4(acc.pp, acc.pm, acc.mp, acc.mm);
+    // segmented inclusive scan (element: the composite, or a reset + identity at a barrier)
+    const bool bar = !exact;   // (all lanes valid: nsb % 256 == 0)
+    C64 m = exact ? acc : c64_id();
+    int fl = bar ? 1 : 0;
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const C64 ym = shfl_up_c64(m, off);
+        const int yf = __shfl_up(fl, off);
+        if (lane >= off) {
+            if (!fl) m = c64_mul(ym, m);
+            fl |= yf;
+        }
+    }
+    __shared__ C64 sWm[kThreads / 64];
+    __shared__ int sWf[kThreads / 64];
+    __shared__ unsigned long long sMask[kThreads / 64];
+    const unsigned long long bmask = __ballot(bar);
+    if (lane == 63) {
+        sWm[wv] = m;
+        sWf[wv] = fl;
+    }
+    if (lane == 0) sMask[wv] = bmask;
+    __syncthreads();
+    C64 before = c64_id();   // the waves before this one
+    for (int w = 0; w < wv; ++w) before = sWf[w] ? sWm[w] : c64_mul(before, sWm[w]);
+    const C64 inc = fl ? m : c64_mul(before, m);
+    C64 ex = shfl_up_c64(inc, 1);
+    if (lane == 0) ex = before;
+    rx[gid] = make_double4(ex.pp, ex.pm, ex.mp, ex.mm);
+    SegSum& sg = seg[blockIdx.x];
+    int fb = -1;   // the segment's first barrier
+#pragma unroll
+    for (int w = kThreads / 64 - 1; w >= 0; --w)
+        if (sMask[w]) fb = w * 64 + (int)__builtin_ctzll(sMask[w]);
+    if ((int)threadIdx.x == fb) sg.lead = make_double4(ex.pp, ex.pm, ex.mp, ex.mm);
+    if (threadIdx.x == kThreads - 1) {
+        sg.tail = make_double4(inc.pp, inc.pm, inc.mp, inc.mm);
+        if (fb < 0) sg.lead = make_double4(inc.pp, inc.pm, inc.mp, inc.mm);
+    }
+    if (threadIdx.x < kThreads / 64) sg.mask[threadIdx.x] = sMask[threadIdx.x];
 }
 
 // K3b: irregular blocks, 16 lanes per block (lane i owns positions [16i, 16i+16)):
@@ -1185,6 +1247,238 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
 #endif
 }
 
+// K4, segment path (one 256-lane workgroup per chunk of 16 segments): the barrier list from
+// the segments' masks, each barrier's gap composite from the K3 summaries (the run before it
+// inside its segment is its rx; a run across segments is the tail of the barrier's segment
+// times the leads of the barrier-free segments between), the serial chain over the barriers
+// (as k_vit_chain), then the anchor values (a barrier's exit, + its post composite for
+// SPLIT) by block id and the entry value of every segment.  Block entries: K5.
+constexpr int kSegT = 256;
+constexpr int kMaxSeg = 16;   // segments per chunk (chunks up to 1 Mi)
+__global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
+    VitConsts vc, const uint32_t* packed, Geo g, const VitPlan* __restrict__ plan,
+    const double4* __restrict__ comp3, const uint8_t* __restrict__ degen,
+    const double4* __restrict__ rx, const SegSum* __restrict__ seg, double2* __restrict__ entry,
+    double2* __restrict__ went, double4* __restrict__ gap, int32_t* __restrict__ barlist,
+    double2* __restrict__ vout, const double2* __restrict__ vhead) {
+    const int64_t c = blockIdx.x;
+    const int t = threadIdx.x;
+    const int nseg = (int)(g.nsb / kThreads);
+    const int64_t s0 = c * nseg;
+    double2* ent = entry + c * (g.nsb + 1);
+    if (degen[c]) {
+        for (int w = t; w < nseg; w += kSegT) went[s0 + w] = make_double2(-DBL_MAX, -DBL_MAX);
+        if (t == 0) ent[g.nsb] = make_double2(-DBL_MAX, -DBL_MAX);
+        return;
+    }
+    const uint32_t* pk = chunk_ptr(packed, g, c);
+    const VitPlan* pl = plan + c * g.nsb;
+    const double4* cp = comp3 + c * g.nsb;                          // SPLIT pre composites
+    const double4* cq = comp3 + (g.nchunks + c) * g.nsb;            // SPLIT post composites
+    const double4* rxc = rx + c * g.nsb;
+    double2* voc = vout + c * g.nsb;
+    double4* gpc = gap + c * g.nsb;
+    int32_t* blc = barlist + c * g.nsb;
+    __shared__ double4 sL[16];
+    __shared__ double4 stepL[kSB];
+    __shared__ double4 stageL[kStageSteps];
+    __shared__ C64 sLead[kMaxSeg], sTail[kMaxSeg];
+    __shared__ int sOff[kMaxSeg * 4 + 1];
+    __shared__ int32_t sBar[kMaxSeg * kThreads];
+    __shared__ int sWoff[kMaxStagedBar + 1];
+    __shared__ int sWa[kMaxStagedBar], sWb[kMaxStagedBar];
+    __shared__ int64_t sWk[kMaxStagedBar];
+    __shared__ C64 sGap[kMaxStagedBar];
+    __shared__ double2 sVo[kMaxStagedBar];
+    if (t < 16) sL[t] = make_double4(vc.L[t][0], vc.L[t][1], vc.L[t][2], vc.L[t][3]);
+    const double2 vhead0 = t == 0 ? vhead[c] : make_double2(0.0, 0.0);
+    // A. barrier list: popcounts of the chunk's mask words, one wave's scan, then every word's
+    //    barriers at their rank
+    const int nwords = nseg * 4;
+    unsigned long long mw = 0;
+    if (t < nwords) mw = seg[s0 + (t >> 2)].mask[t & 3];
+    if (t < nseg) {
+        sLead[t] = ld_c64(&seg[s0 + t].lead);
+        sTail[t] = ld_c64(&seg[s0 + t].tail);
+    }
+    if (t < 64) {
+        const int cnt = (int)__popcll(mw);
+        int x = cnt;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d);
+            if (t >= d) x += y;
+        }
+        if (t < nwords) sOff[t] = x - cnt;
+        if (t == 63) sOff[nwords] = x;
+    }
+    __syncthreads();
+    const int nbar = sOff[nwords];
+    if (t < nwords) {
+        int o = sOff[t];
+        const int base = (t >> 2) * kThreads + (t & 3) * 64;
+        while (mw) {
+            sBar[o++] = base + (int)__builtin_ctzll(mw);
+            mw &= mw - 1;
+        }
+    }
+    __syncthreads();
+    // B. gap composites and windows, one lane per barrier
+    for (int i = t; i < nbar; i += kSegT) {
+        const int k = sBar[i];
+        const VitPlan p = pl[k];
+        C64 R = c64_id();
+        if (i > 0) {
+            const int kp = sBar[i - 1], sp = kp / kThreads, sk = k / kThreads;
+            if (sp == sk) {
+                R = ld_c64(rxc + k);
+            } else {
+                R = sTail[sp];
+                for (int u = sp + 1; u < sk; ++u) R = c64_mul(R, sLead[u]);
+                R = c64_mul(R, ld_c64(rxc + k));
+            }
+            if (pl[kp].type == PLAN_SPLIT) R = c64_mul(ld_c64(cq + kp), R);
+            if (p.type == PLAN_SPLIT) R = c64_mul(R, ld_c64(cp + k));
+        }
+        int ja = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
+        int jb = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
+        if (k == 0) ja = jb = 0;   // block 0: walked by K2's head lanes
+        blc[i] = k;
+        st_c64(gpc + i, R);
+        if (i < kMaxStagedBar) {
+            sWk[i] = k;
+            sWa[i] = ja;
+            sWb[i] = jb;
+            sGap[i] = R;
+        }
+    }
+    __syncthreads();
+    // C. the serial chain over the barriers (k_vit_chain's phase 3)
+    const uint32_t o0 = base_at(pk, 0);
+    const double2 init = make_double2(vc.logpi[o0], vc.logpi[o0 + 4]);
+    const int nst = min(nbar, kMaxStagedBar);
+    if (t == 0) {
+        int o = 0;
+        for (int i = 0; i < nst; ++i) {
+            sWoff[i] = o;
+            const int len = max(0, sWb[i] - sWa[i]);
+            o = (o + len <= kStageSteps) ? o + len : kStageSteps + 1;   // overflow marker
+        }
+        sWoff[nst] = o;
+    }
+    __syncthreads();
+    for (int i = t >> 6; i < nst; i += kSegT / 64) {   // one wave per window
+        const int off = sWoff[i];
+        const int len = max(0, sWb[i] - sWa[i]);
+        if (off + len > kStageSteps) continue;
+        for (int j = t & 63; j < len; j += 64) {
+            const int64_t pos = sWk[i] * kSB + sWa[i] + j;
+            const uint32_t d = base_at(pk, pos - 1) | (base_at(pk, pos) << 2);
+            stageL[off + j] = sL[d];
+        }
+    }
+    __syncthreads();
+    const bool all_staged = nst == nbar && sWoff[nst] <= kStageSteps;
+    if (all_staged) {
+        if (t == 0) {
+            double2 v = init;
+            int i0 = 0;
+            if (nbar > 0 && sWk[0] == 0) {   // block 0 (always the first barrier)
+                v = vhead0;
+                voc[0] = v;
+                sVo[0] = v;
+                i0 = 1;
+            }
+            int offn = 0, lenn = 0;
+            C64 gapn = c64_id();
+            if (i0 < nbar) {
+                offn = sWoff[i0];
+                lenn = sWb[i0] - sWa[i0];
+                gapn = sGap[i0];
+            }
+            for (int i = i0; i < nbar; ++i) {
+                const int off = offn, len = lenn;
+                const C64 gp = gapn;
+                if (i + 1 < nbar) {
+                    offn = sWoff[i + 1];
+                    lenn = sWb[i + 1] - sWa[i + 1];
+                    gapn = sGap[i + 1];
+                }
+                v = c64_apply(v, gp);
+                double P = v.x, M = v.y;
+                const double4* st = stageL + off;
+#pragma unroll 8
+                for (int j = 0; j < len; ++j) {
+                    const double4 l = st[j];
+                    const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
+                    P = s.P;
+                    M = s.M;
+                }
+                v = make_double2(P, M);
+                voc[i] = v;
+                sVo[i] = v;
+            }
+        }
+    } else if (t < 64) {
+        double2 v = init;
+        for (int i = 0; i < nbar; ++i) {
+            if (i == 0 && sBar[0] == 0) {   // block 0 (always the first barrier)
+                v = vhead[c];
+            } else if (i < nst && sWoff[i] + max(0, sWb[i] - sWa[i]) <= kStageSteps) {
+                v = c64_apply(v, sGap[i]);
+                if (t == 0) {
+                    double P = v.x, M = v.y;
+                    const double4* st = stageL + sWoff[i];
+                    const int len = sWb[i] - sWa[i];
+#pragma unroll 8
+                    for (int j = 0; j < len; ++j) {
+                        const double4 l = st[j];
+                        const Step s = ref_step(P, M, l.x, l.y, l.z, l.w);
+                        P = s.P;
+                        M = s.M;
+                    }
+                    v = make_double2(P, M);
+                }
+                v = make_double2(__shfl(v.x, 0), __shfl(v.y, 0));
+            } else {
+                const int64_t k = blc[i];
+                const VitPlan p = pl[k];
+                v = c64_apply(v, ld_c64(gpc + i));
+                const int ja = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
+                const int jb = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
+                v = chain_window(pk, sL, stepL, k, ja, jb, v, t);
+            }
+            if (t == 0) {
+                voc[i] = v;
+                if (i < kMaxStagedBar) sVo[i] = v;
+            }
+        }
+    }
+    __syncthreads();
+    // D. anchor values by block id: the barrier's exit (SPLIT: + the post composite)
+    auto anchor_val = [&](int i) {
+        const int k = sBar[i];
+        double2 v = i < kMaxStagedBar ? sVo[i] : voc[i];
+        if (pl[k].type == PLAN_SPLIT) v = c64_apply(v, ld_c64(cq + k));
+        return v;
+    };
+    for (int i = t; i < nbar; i += kSegT) ent[sBar[i]] = anchor_val(i);
+    // E. segment entries (segment 0: the initial value; block 0 is its first barrier) and the
+    //    chunk's final value (K6)
+    if (t <= nseg) {
+        double2 E = init;
+        if (t > 0) {
+            const int il = sOff[4 * t] - 1;   // the last barrier before segment t (>= block 0)
+            const int kl = sBar[il], sl = kl / kThreads;
+            C64 R = sTail[sl];
+            for (int u = sl + 1; u < t; ++u) R = c64_mul(R, sLead[u]);
+            E = c64_apply(anchor_val(il), R);
+        }
+        if (t < nseg) went[s0 + t] = E;
+        else ent[g.nsb] = E;
+    }
+}
+
 // ---------------------------------------------------------------- K5: re-forward
 __device__ __forceinline__ uint32_t map_apply(uint32_t m, uint32_t x) { return (m >> x) & 1u; }
 __device__ __forceinline__ uint32_t map_compose(uint32_t f, uint32_t g) {   // f o g
@@ -1222,7 +1516,10 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
                                                           const double2* __restrict__ entry,
                                                           uint4* __restrict__ bp,
                                                           uint8_t* __restrict__ origin,
-                                                          uint32_t* status) {
+                                                          uint32_t* status,
+                                                          const double4* __restrict__ rx,
+                                                          const SegSum* __restrict__ seg,
+                                                          const double2* __restrict__ went) {
     // conflict-free halves (16 x 16 B each); entry 16 is the identity step (0, -inf, -inf,
     // 0) standing for block 0's position 0: P + 0.0 = P and M + -inf = -inf exactly, so the
     // values, the tie bits that matter and the origins are unchanged by it
@@ -1249,7 +1546,35 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
     }
     const uint32_t* pk = chunk_ptr(packed, g, c);
     const double2* ent = entry + c * (g.nsb + 1);
-    const double2 v0 = ent[k];
+    double2 v0, vnext;   // this block's entry, the next block's (the self-check)
+    if (seg) {
+        // segment path (workgroup = segment): entry = anchor value . rx, the anchor being the
+        // last barrier before the block in the segment (K4's value by block id) or, with none,
+        // the segment's entry
+        const int l = threadIdx.x;
+        const SegSum& sg = seg[blockIdx.x];
+        const unsigned long long m[4] = {sg.mask[0], sg.mask[1], sg.mask[2], sg.mask[3]};
+        const int q = l >> 6, r = l & 63;
+        const unsigned long long mq = q == 0 ? m[0] : q == 1 ? m[1] : q == 2 ? m[2] : m[3];
+        int a = -1;
+#pragma unroll
+        for (int qq = 0; qq < 4; ++qq)
+            if (qq < q && m[qq]) a = qq * 64 + 63 - (int)__builtin_clzll(m[qq]);
+        const unsigned long long below = r ? (mq & ((1ull << r) - 1ull)) : 0ull;
+        if (below) a = q * 64 + 63 - (int)__builtin_clzll(below);
+        const int64_t sbase = k - l;
+        const double2 E = went[blockIdx.x];
+        v0 = c64_apply(a >= 0 ? ent[sbase + a] : E, ld_c64(rx + gid));
+        if (l + 1 < kThreads) {
+            const int a2 = ((mq >> r) & 1ull) ? l : a;
+            vnext = c64_apply(a2 >= 0 ? ent[sbase + a2] : E, ld_c64(rx + gid + 1));
+        } else {
+            vnext = k + 1 == g.nsb ? ent[g.nsb] : went[blockIdx.x + 1];
+        }
+    } else {
+        v0 = ent[k];
+        vnext = ent[k + 1];
+    }
     double P = v0.x, M = v0.y;
     uint32_t oP = 1u, oM = 0u;   // origin sign of the current '+' / '-' survivor
     uint32_t wP0 = 0, wP1 = 0, wM0 = 0, wM1 = 0;
@@ -1339,7 +1664,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
         }
     }
     origin[gid] = (uint8_t)(oM | (oP << 1));
-    const double2 nx = ent[k + 1];
+    const double2 nx = vnext;
     if (__double_as_longlong(nx.x) != __double_as_longlong(P) ||
         __double_as_longlong(nx.y) != __double_as_longlong(M))
         atomicOr(status, ST_VERIFY_ENTRY);
@@ -1492,6 +1817,8 @@ struct VitWs {
     uint8_t* origin;
     uint8_t* endst;
     uint8_t* degen;
+    SegSum* seg;      // segment path: per 256-block segment
+    double2* went;    // segment entries
     size_t bytes;
 };
 
@@ -1522,6 +1849,8 @@ VitWs carve(void* base, int64_t nchunks, int64_t nsb) {
     w.origin = (uint8_t*)take(nt);
     w.endst = (uint8_t*)take(nt);
     w.degen = (uint8_t*)take(nchunks);
+    w.seg = (SegSum*)take((nt / kThreads + 1) * sizeof(SegSum));
+    w.went = (double2*)take((nt / kThreads + 1) * sizeof(double2));
     w.bytes = off + 256;
     return w;
 }
@@ -1555,14 +1884,23 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     const size_t nbz = (size_t)(vc.emax - vc.emin + 1);
     const size_t lds3x = (nbz * 16 * 2 + std::max(nbz * 64 * 2, (size_t)kW4 * 2)) * sizeof(double2);
     // K3 + K3b in one launch: the chunks' irregular blocks run as extra workgroups
+    // the segment path for chunks of whole 256-block segments, at most kMaxSeg of them (the
+    // reference's 1 Mi decode chunk: 16); rx in the gk slot
+    const bool segp = nsb % kThreads == 0 && nsb / kThreads <= kMaxSeg && chunk_len == nsb * kSB;
+    SegSum* sg = segp ? w.seg : nullptr;
     hipLaunchKernelGGL(k_vit_exact, dim3(grid + (unsigned)nchunks), dim3(kThreads), lds3x, s, vc,
                        d_vt, packed, g, w.plan, w.comp3, status, grid, w.aent, w.splitlist,
-                       w.splitcount);
-    hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kChainT), 0, s, vc, packed, g,
-                       w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout,
-                       w.vhead);
+                       w.splitcount, w.gk, sg);
+    if (segp)
+        hipLaunchKernelGGL(k_vit_chain_seg, dim3((unsigned)nchunks), dim3(kSegT), 0, s, vc, packed,
+                           g, w.plan, w.comp3, w.degen, w.gk, sg, w.entry, w.went, w.gap,
+                           w.barlist, w.vout, w.vhead);
+    else
+        hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kChainT), 0, s, vc, packed,
+                           g, w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout,
+                           w.vhead);
     hipLaunchKernelGGL(k_vit_forward, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.degen,
-                       w.entry, w.bp, w.origin, status);
+                       w.entry, w.bp, w.origin, status, w.gk, sg, w.went);
     hipLaunchKernelGGL(k_vit_tscan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, g, w.entry,
                        w.origin, w.endst, score);
     hipLaunchKernelGGL(k_vit_trace, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst, sign_out,
