@@ -7,6 +7,8 @@
 #include <cstring>
 #include <vector>
 
+#include <atomic>
+
 #include "cpg_internal.h"
 
 namespace cpg {
@@ -29,6 +31,14 @@ int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
     }
     *out = b.p;
     return CPG_OK;
+}
+
+uint32_t lookback_epoch() {
+    static std::atomic<uint32_t> ctr{0};
+    for (;;) {
+        const uint32_t e = (++ctr) * 0x9E3779B1u;
+        if (e != 0u && e != 0xFFFFFFFFu) return e;
+    }
 }
 
 int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
@@ -186,6 +196,8 @@ int cpg_reserve(cpg_ctx* ctx, int64_t nbases) {
     if ((rc = ws_get(ctx, WS_COUNT, count_ws_bytes(nt), &p))) return rc;
     if ((rc = ws_get(ctx, WS_VIT, viterbi_ws_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
+    if ((rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
+    if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nd + 1) * 8, &p))) return rc;
     if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nt, CPG_TRAIN_CHUNK), &p))) return rc;
     return CPG_OK;
 }
@@ -216,6 +228,10 @@ int cpg_sync(cpg_ctx* ctx, void* stream) {
     if (st) {
         CPG_HIP(hipMemsetAsync(ctx->d_status, 0, 4, s));
         CPG_HIP(hipStreamSynchronize(s));
+        if (st & ST_VIT_LOOKBACK)
+            return set_error(CPG_E_DEVICE,
+                             "viterbi: the look-back over a chunk's earlier segments timed out; "
+                             "the decoded path is unusable (status 0x%x)", st);
         if (st & ST_LOOKBACK_TIMEOUT)
             return set_error(CPG_E_DEVICE,
                              "island records: the look-back over earlier chunks' counts timed "
@@ -281,9 +297,11 @@ int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed
     void* ws;
     const size_t need = viterbi_ws_bytes(nch, chunk_len);
     if ((rc = ws_get(ctx, WS_VIT, need, &ws))) return rc;
+    void* agg;
+    if ((rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(nch, chunk_len), &agg))) return rc;
     CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
-                           d_sign_out, d_score, nullptr, ctx->d_status, s, d_sign_out + w_done,
-                           ntail));
+                           d_sign_out, d_score, nullptr, ctx->d_status, s,
+                           static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail));
     return CPG_OK;
 }
 
@@ -299,8 +317,11 @@ int cpg_islands_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign
     const int64_t nch = nbases / chunk_len;
     void* ws;
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &ws))) return rc;
+    void* fl;
+    if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nch + 1) * 8, &fl))) return rc;
     CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, 0, ws, ctx->ws[WS_ISL].bytes, d_out,
-                           cap, d_count, ctx->d_status, pick(ctx, stream)));
+                           cap, d_count, ctx->d_status, pick(ctx, stream),
+                           static_cast<unsigned long long*>(fl)));
     return CPG_OK;
 }
 
@@ -316,9 +337,11 @@ int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_s
     const int64_t nch = nbases / chunk_len;
     void* ws;
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &ws))) return rc;
+    void* fl;
+    if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nch + 1) * 8, &fl))) return rc;
     CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, first_chunk, ws,
                            ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status,
-                           pick(ctx, stream)));
+                           pick(ctx, stream), static_cast<unsigned long long*>(fl)));
     return CPG_OK;
 }
 

@@ -32,6 +32,7 @@ enum : uint32_t {
     ST_VERIFY_CHAIN = 1u << 2,   // K7 traceback start state mismatch
     ST_CONTIG_LAYOUT = 1u << 3,  // a contig breaks the batch layout contract (skipped)
     ST_LOOKBACK_TIMEOUT = 1u << 4,   // a bounded look-back spin gave up (records unusable)
+    ST_VIT_LOOKBACK = 1u << 5,       // the Viterbi segment look-back gave up (path unusable)
 };
 
 // ---- Viterbi constants (host-computed, shared by every kernel) ---------------------
@@ -110,6 +111,18 @@ struct Buf {
     size_t bytes = 0;
 };
 
+// ---- workspace slots (cpg_ctx::ws) ------------------------------------------------
+enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
+       WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9, WS_GEN = 10, WS_GISL = 11, WS_CSORT = 12,
+       WS_CBP = 13, WS_CISL = 14, WS_CCK = 15,
+       // look-back words tagged with a per-call epoch (Viterbi segment products, island
+       // counts): slots of their own, so that stale words are only older tags — never other
+       // arrays of a differently laid-out earlier call whose bits could pass for the tag
+       WS_VAGG = 16, WS_IFLG = 17, WS_NSLOT = 18 };
+// a fresh look-back tag per call: an odd multiple of a counter (a bijection: distinct for 2^32
+// calls), never 0 (zero-filled workspace) or all ones
+uint32_t lookback_epoch();
+
 }  // namespace cpg
 
 struct cpg_ctx {
@@ -118,7 +131,7 @@ struct cpg_ctx {
     std::mutex mu;
     uint32_t* d_status = nullptr;     // device status word
     // workspace (grown on demand; cpg_reserve pre-sizes)
-    cpg::Buf ws[16];
+    cpg::Buf ws[cpg::WS_NSLOT];
     // host staging (pinned)
     cpg::Buf pin[4];
     // device copies of per-model Viterbi tables
@@ -149,9 +162,6 @@ bool aligned16(const void* p);
 int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitConsts& vc, const VitTables& vt,
                const VitTables** out);
 int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out);
-enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
-       WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9, WS_GEN = 10, WS_GISL = 11, WS_CSORT = 12,
-       WS_CBP = 13, WS_CISL = 14, WS_CCK = 15 };
 int vit_prepare(const cpg_model* m, int64_t chunk_len, VitConsts* vc, VitTables* vt);
 
 // kernel launchers (defined in the .hip files); all asynchronous on `s`
@@ -166,9 +176,10 @@ size_t count_ws_bytes(int64_t nchunks);
 hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint32_t* packed,
                           int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
                           uint32_t* sign_out, double* score, uint8_t* degen,
-                          uint32_t* status, hipStream_t s, uint32_t* zero_at = nullptr,
-                          int64_t zero_n = 0);
+                          uint32_t* status, hipStream_t s, unsigned long long* agg,
+                          uint32_t* zero_at = nullptr, int64_t zero_n = 0);
 size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len);
+size_t viterbi_agg_bytes(int64_t nchunks, int64_t chunk_len);   // WS_VAGG
 // model-derived LDS tables of K1/K3, built once per model right after the VitTables copy
 size_t vit_derived_bytes();
 hipError_t launch_vit_tables(const VitConsts& vc, VitTables* d_vt, hipStream_t s);
@@ -176,7 +187,8 @@ int64_t vit_nsb(int64_t chunk_len);
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* ws, size_t ws_bytes,
                           cpg_island* out, int64_t cap, int64_t* count, uint32_t* status,
-                          hipStream_t s, const int64_t* base_in = nullptr);
+                          hipStream_t s, unsigned long long* flags,
+                          const int64_t* base_in = nullptr);   // flags: WS_IFLG, nchunks words
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
 // gtab: the model's one-step tables in device memory (est_tables); needed with PART_ACC
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,

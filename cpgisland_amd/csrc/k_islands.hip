@@ -123,7 +123,7 @@ IslWs carve_isl(void* base, int64_t nchunks, int64_t C) {
     w.ttot = (Cnt5*)take(nt * sizeof(Cnt5));
     w.toff = (Cnt5*)take(nt * sizeof(Cnt5));
     w.kept = (int32_t*)take(nchunks * maxr * 4);
-    w.flags = (unsigned long long*)take(nchunks * 8);
+    w.flags = nullptr;   // WS_IFLG (launch_islands)
     w.bytes = o + 256;
     return w;
 }
@@ -581,19 +581,18 @@ size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len) {
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* wsp, size_t ws_bytes,
                           cpg_island* out, int64_t cap, int64_t* count, uint32_t* status,
-                          hipStream_t s, const int64_t* base_in) {
+                          hipStream_t s, unsigned long long* flags, const int64_t* base_in) {
     IslWs ws = carve_isl(wsp, nchunks, chunk_len);
-    if (ws.bytes > ws_bytes) return hipErrorInvalidValue;
+    if (ws.bytes > ws_bytes || !flags) return hipErrorInvalidValue;
+    ws.flags = flags;
     if (nchunks == 0)
         return base_in ? hipMemcpyAsync(count, base_in, sizeof(int64_t), hipMemcpyDeviceToDevice, s)
                        : hipMemsetAsync(count, 0, sizeof(int64_t), s);
     hipLaunchKernelGGL(k_isl_tile, dim3((unsigned)(nchunks * ws.ntile)), dim3(kTT), 0, s, packed,
                        sign, chunk_len, ws);
-    // a fresh tag per call for the look-back flags (stale flags of earlier calls never match)
-    static std::atomic<uint32_t> epoch_ctr{0};
-    uint32_t epoch = ++epoch_ctr;
-    if (epoch == 0) epoch = ++epoch_ctr;
-    const IslOut o{out, cap, count, base_in, first_chunk, epoch, status};
+    // a fresh tag per call for the look-back flags (their own workspace slot: stale words are
+    // earlier calls' flags, whose tags never match)
+    const IslOut o{out, cap, count, base_in, first_chunk, lookback_epoch(), status};
     hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed,
                        chunk_len, ws, o);
     return hipGetLastError();

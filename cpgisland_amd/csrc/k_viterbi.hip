@@ -38,6 +38,7 @@
 // Dinucleotide code d = prev | cur << 2 (one bfe of the packed word).
 
 #include <algorithm>
+#include <atomic>
 #include <cfloat>
 #include <cmath>
 
@@ -47,6 +48,7 @@ namespace cpg {
 namespace {
 
 constexpr int kThreads = 256;
+constexpr int kMaxSeg = 16;   // segment path: 256-block segments per chunk (chunks up to 1 Mi)
 constexpr int32_t kNeg32 = -(1 << 30);
 constexpr int64_t kNeg64 = -(1ll << 60);
 
@@ -328,9 +330,34 @@ __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables
     }
 }
 
+// Segment path of K1 (chunks of whole 256-block segments): K2's work folded in.  Each
+// workgroup (one segment) scans its blocks' approximate composites, publishes the segment's
+// product as 8 epoch-tagged 64-bit words (no fence needed: every word validates itself),
+// multiplies the products of the chunk's earlier segments (a look-back: workgroups start in
+// order, so every segment waited on is running or done; the spin is bounded) into its entry
+// estimate, and classifies its own blocks.  Irregular blocks go to a per-segment list.
+struct ApproxSeg {
+    unsigned long long* agg;   // [segment][8]: epoch << 32 | 32-bit half of the product
+    uint32_t epoch;
+    longlong2* aent;
+    uint8_t* degen;
+    VitPlan* plan;
+    int32_t* irrlist;          // [segment][256]
+    int32_t* irrseg;           // [segment]: irregular blocks listed
+    uint32_t* status;
+};
+#ifndef CPG_VIT_SPIN_LIMIT
+#define CPG_VIT_SPIN_LIMIT 200000000ull   // 2 s of the 100 MHz wall clock
+#endif
+__device__ void approx_segment(const VitConsts& vc, const Geo& g, const uint32_t* pk, int64_t c,
+                               int64_t k, CI x, const ApproxSeg& as);
+__device__ __forceinline__ int64_t fix_of(double x, int f);
+__device__ __forceinline__ VitPlan classify(const VitConsts& vc, const Geo& g, int64_t k,
+                                            longlong2 en, longlong2 ex, bool& irregular);
+
 __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uint32_t* packed,
                                                          Geo g, const VitTables* vt,
-                                                         int4* __restrict__ comp) {
+                                                         int4* __restrict__ comp, ApproxSeg as) {
     __shared__ int4 Q[16];
     // 4-step products over 5-base windows b0..b4 (exact: integers) [0, 1024), then the
     // 3-step products of steps 1..3 over b1..b4 [1024, 1280): block 0's first window (the
@@ -344,7 +371,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uin
     for (int i = 0; i < kQ4 / kThreads; ++i) Q4[threadIdx.x + i * kThreads] = gq[threadIdx.x + i * kThreads];
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (gid >= g.nchunks * g.nsb) return;
+    if (gid >= g.nchunks * g.nsb) return;   // (segment path: every lane is valid)
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     const uint32_t* pk = chunk_ptr(packed, g, c);
     if (g.whole(k)) {
@@ -360,6 +387,10 @@ __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uin
                 return (j == 0 && first) ? 1024u + (wi >> 2) : wi;
             },
             [&](uint32_t wi) { return Q4[wi]; }, [&](const int4 q, int) { acc = i4_mul(acc, q); });
+        if (as.agg) {   // segment path (whole blocks only)
+            approx_segment(vc, g, pk, c, k, CI{acc.x, acc.y, acc.z, acc.w}, as);
+            return;
+        }
         comp[gid] = acc;
         return;
     }
@@ -505,6 +536,94 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
     if (t == 0) irrcount[c] = sIrr;
 }
 
+// K1's segment path after the block composite x (see ApproxSeg)
+__device__ void approx_segment(const VitConsts& vc, const Geo& g, const uint32_t* pk, int64_t c,
+                               int64_t k, CI x, const ApproxSeg& as) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int sidx = (int)(k / kThreads);   // segment within the chunk (workgroup-uniform)
+    const uint32_t o0 = base_at(pk, 0);
+    const double lp = vc.logpi[o0], lm = vc.logpi[o0 + 4];
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + t;
+    if (!(lp > -INFINITY) && !(lm > -INFINITY)) {   // DEGEN chunk (uniform)
+        as.plan[gid] = VitPlan{PLAN_DEGEN, 0, 0, 0, 0, 0};
+        if (t == 0) {
+            as.irrseg[blockIdx.x] = 0;
+            if (sidx == 0) as.degen[c] = 1;
+        }
+        return;
+    }
+    if (t == 0 && sidx == 0) as.degen[c] = 0;
+    // inclusive scan of the segment's composites (exact integer max-plus)
+    CI s = x;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const CI y = shfl_up_ci(s, off);
+        if (lane >= off) s = ci_mul(y, s);
+    }
+    __shared__ CI sW[kThreads / 64];
+    __shared__ unsigned long long sPre[16 * 8];
+    __shared__ longlong2 sEnt;
+    __shared__ int sIrr;
+    if (lane == 63) sW[wv] = s;
+    if (t == 0) sIrr = 0;
+    __syncthreads();
+    CI before = ci_id();
+    for (int w = 0; w < wv; ++w) before = ci_mul(before, sW[w]);
+    const CI up = shfl_up_ci(s, 1);
+    const CI excl = lane > 0 ? ci_mul(before, up) : before;
+    // publish the segment's product, then read the earlier segments' (this call's epoch)
+    if (t < 8) {
+        const CI tot = ci_mul(ci_mul(sW[0], sW[1]), ci_mul(sW[2], sW[3]));
+        const int64_t v = (t >> 1) == 0 ? tot.pp : (t >> 1) == 1 ? tot.pm : (t >> 1) == 2 ? tot.mp : tot.mm;
+        const uint32_t half = (t & 1) ? (uint32_t)((uint64_t)v >> 32) : (uint32_t)v;
+        __hip_atomic_store(as.agg + (int64_t)blockIdx.x * 8 + t,
+                           ((unsigned long long)as.epoch << 32) | half, __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (t < 8 * sidx) {
+        const unsigned long long* src = as.agg + ((int64_t)blockIdx.x - sidx + (t >> 3)) * 8 + (t & 7);
+        const unsigned long long t0 = wall_clock64();
+        unsigned long long f;
+        for (;;) {
+            f = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(f >> 32) == as.epoch) break;
+            if (wall_clock64() - t0 >= (unsigned long long)(CPG_VIT_SPIN_LIMIT)) {
+                atomicOr(as.status, ST_VIT_LOOKBACK);
+                f = 0;
+                break;
+            }
+            __builtin_amdgcn_s_sleep(1);
+        }
+        sPre[t] = f;
+    }
+    __syncthreads();
+    if (t == 0) {   // the segment's entry estimate: the chunk's start times the earlier products
+        const int f = vc.qshift;
+        int64_t P = fix_of(lp, f), M = fix_of(lm, f);
+        for (int j = 0; j < sidx; ++j) {
+            const unsigned long long* w = sPre + 8 * j;
+            auto val = [&](int i) {
+                return (int64_t)(((uint64_t)(uint32_t)w[2 * i + 1] << 32) | (uint32_t)w[2 * i]);
+            };
+            ci_apply(P, M, CI{val(0), val(1), val(2), val(3)});
+        }
+        sEnt = make_longlong2(P, M);
+    }
+    __syncthreads();
+    int64_t P = sEnt.x, M = sEnt.y;
+    ci_apply(P, M, excl);
+    const longlong2 en = make_longlong2(P, M);
+    ci_apply(P, M, x);
+    bool irregular;
+    as.plan[gid] = classify(vc, g, k, en, make_longlong2(P, M), irregular);
+    if (irregular) {
+        as.aent[c * (g.nsb + 1) + k] = en;
+        as.irrlist[(int64_t)blockIdx.x * kThreads + atomicAdd(&sIrr, 1)] = (int32_t)k;
+    }
+    __syncthreads();
+    if (t == 0) as.irrseg[blockIdx.x] = sIrr;
+}
+
 // ---------------------------------------------------------------- K3: exact composites
 // comp3: the pre composites of all blocks [nchunks * nsb], then the post composites [same];
 // a block's post is written (and read) for SPLIT blocks only, so K4's one workgroup per chunk
@@ -523,7 +642,7 @@ __device__ void vit_irregular(const VitConsts& vc, const uint32_t* packed, const
                               const int32_t* __restrict__ irrlist,
                               const int32_t* __restrict__ irrcount,
                               double4* __restrict__ comp3, int64_t c, const double2* sA,
-                              const double2* sB);
+                              const double2* sB, const int32_t* __restrict__ irrseg);
 
 // Segment path (chunks of a multiple of 256 blocks, e.g. 1 Mi): each regular workgroup (256
 // blocks of one chunk = one "segment") also runs a segmented scan of its exact composites,
@@ -550,7 +669,9 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
                                                         const int32_t* __restrict__ irrlist,
                                                         const int32_t* __restrict__ irrcount,
                                                         double4* __restrict__ rx,
-                                                        SegSum* __restrict__ seg) {
+                                                        SegSum* __restrict__ seg,
+                                                        const int32_t* __restrict__ irrseg,
+                                                        double2* __restrict__ vhead) {
     // per binade slot: single-step halves sA/sB [16] (one 256-B bank row each) and 2-step
     // composites over 3-base windows, halves P2A = (pp, pm), P2B = (mp, mm) [64].  Every
     // entry is a sum of binade-rounded constants: exact on the binade's grid.
@@ -574,11 +695,16 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
             sB[i] = dv->sB[vc.emin * 16 + i];
         }
     };
+    if (blockIdx.x >= main_grid + g.nchunks) {   // segment path: block 0's walk (K2's heads)
+        vit_head(vc, packed, g,
+                 (int64_t)(blockIdx.x - main_grid - g.nchunks) * kThreads + threadIdx.x, vhead);
+        return;
+    }
     if (blockIdx.x >= main_grid) {   // workgroup-uniform: the chunk's irregular blocks
         load_single();
         __syncthreads();
         vit_irregular(vc, packed, g, aent, plan, irrlist, irrcount, comp3,
-                      (int64_t)(blockIdx.x - main_grid), sA, sB);
+                      (int64_t)(blockIdx.x - main_grid), sA, sB, irrseg);
         return;
     }
     if (threadIdx.x == 0) {
@@ -748,9 +874,23 @@ __device__ void vit_irregular(const VitConsts& vc, const uint32_t* packed, const
                               const int32_t* __restrict__ irrlist,
                               const int32_t* __restrict__ irrcount,
                               double4* __restrict__ comp3, int64_t c, const double2* sA,
-                              const double2* sB) {
+                              const double2* sB, const int32_t* __restrict__ irrseg) {
     __shared__ int4 Q[16];
-    const int n = irrcount[c];
+    // segment path: the chunk's segments' lists (K1), concatenated through their offsets
+    __shared__ int sOffI[kMaxSeg + 1];
+    const int nseg = (int)(g.nsb / kThreads);
+    if (irrseg) {
+        if (threadIdx.x == 0) {
+            int o = 0;
+            for (int j = 0; j < nseg; ++j) {
+                sOffI[j] = o;
+                o += irrseg[c * nseg + j];
+            }
+            sOffI[nseg] = o;
+        }
+        __syncthreads();
+    }
+    const int n = irrseg ? sOffI[nseg] : irrcount[c];
     if (n == 0) return;   // workgroup-uniform
     const int nb = vc.emax - vc.emin + 1;
     if (threadIdx.x < 16)
@@ -765,7 +905,14 @@ __device__ void vit_irregular(const VitConsts& vc, const uint32_t* packed, const
     const int group = threadIdx.x >> 4;             // 16 groups per workgroup
     for (int it = group; it < n; it += 16) {
         (void)gbase;
-        const int64_t k = irrlist[c * g.nsb + it];
+        int64_t k;
+        if (irrseg) {
+            int j = 0;
+            while (j + 1 < nseg && sOffI[j + 1] <= it) ++j;
+            k = irrlist[(c * nseg + j) * kThreads + (it - sOffI[j])];
+        } else {
+            k = irrlist[c * g.nsb + it];
+        }
         const int64_t gid = c * g.nsb + k;
         const int j0 = g.jfirst(k), jend = g.jend(k);
         const longlong2 en = aent[c * (g.nsb + 1) + k];
@@ -1254,7 +1401,6 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
 // (as k_vit_chain), then the anchor values (a barrier's exit, + its post composite for
 // SPLIT) by block id and the entry value of every segment.  Block entries: K5.
 constexpr int kSegT = 256;
-constexpr int kMaxSeg = 16;   // segments per chunk (chunks up to 1 Mi)
 __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
     VitConsts vc, const uint32_t* packed, Geo g, const VitPlan* __restrict__ plan,
     const double4* __restrict__ comp3, const uint8_t* __restrict__ degen,
@@ -1819,6 +1965,7 @@ struct VitWs {
     uint8_t* degen;
     SegSum* seg;      // segment path: per 256-block segment
     double2* went;    // segment entries
+    int32_t* irrseg;           // per segment: irregular blocks listed
     size_t bytes;
 };
 
@@ -1851,6 +1998,7 @@ VitWs carve(void* base, int64_t nchunks, int64_t nsb) {
     w.degen = (uint8_t*)take(nchunks);
     w.seg = (SegSum*)take((nt / kThreads + 1) * sizeof(SegSum));
     w.went = (double2*)take((nt / kThreads + 1) * sizeof(double2));
+    w.irrseg = (int32_t*)take((nt / kThreads + 1) * sizeof(int32_t));
     w.bytes = off + 256;
     return w;
 }
@@ -1859,6 +2007,10 @@ VitWs carve(void* base, int64_t nchunks, int64_t nsb) {
 
 int64_t vit_nsb(int64_t chunk_len) { return chunk_len <= 1 ? 1 : (chunk_len + kSB - 1) / kSB; }
 
+size_t viterbi_agg_bytes(int64_t nchunks, int64_t chunk_len) {
+    return (size_t)(nchunks * vit_nsb(chunk_len) / kThreads + 1) * 8 * sizeof(unsigned long long);
+}
+
 size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len) {
     return carve(nullptr, nchunks, vit_nsb(chunk_len)).bytes;
 }
@@ -1866,7 +2018,8 @@ size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len) {
 hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint32_t* packed,
                           int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
                           uint32_t* sign_out, double* score, uint8_t* degen_out,
-                          uint32_t* status, hipStream_t s, uint32_t* zero_at, int64_t zero_n) {
+                          uint32_t* status, hipStream_t s, unsigned long long* agg,
+                          uint32_t* zero_at, int64_t zero_n) {
     const int64_t nsb = vit_nsb(chunk_len);
     VitWs w = carve(ws, nchunks, nsb);
     if (w.bytes > ws_bytes) return hipErrorInvalidValue;
@@ -1877,20 +2030,31 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     // a 256-step dependent chain (~13 us) that set K1's duration; K2 takes as long without it
     // (as K3's extra workgroups it cost K3 0.9 us more: measured, not kept)
     const unsigned head = (unsigned)((nchunks + kScanT - 1) / kScanT);
-    hipLaunchKernelGGL(k_vit_approx, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, d_vt,
-                       w.comp1);
-    hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks + head), dim3(kScanT), 0, s, vc, packed,
-                       g, w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount, w.vhead);
-    const size_t nbz = (size_t)(vc.emax - vc.emin + 1);
-    const size_t lds3x = (nbz * 16 * 2 + std::max(nbz * 64 * 2, (size_t)kW4 * 2)) * sizeof(double2);
-    // K3 + K3b in one launch: the chunks' irregular blocks run as extra workgroups
     // the segment path for chunks of whole 256-block segments, at most kMaxSeg of them (the
-    // reference's 1 Mi decode chunk: 16); rx in the gk slot
+    // reference's 1 Mi decode chunk: 16): K2 folded into K1 (segment scans + look-back), block
+    // 0's walk in K3's launch, K4 over barriers and segment summaries only; rx in the gk slot
     const bool segp = nsb % kThreads == 0 && nsb / kThreads <= kMaxSeg && chunk_len == nsb * kSB;
     SegSum* sg = segp ? w.seg : nullptr;
-    hipLaunchKernelGGL(k_vit_exact, dim3(grid + (unsigned)nchunks), dim3(kThreads), lds3x, s, vc,
-                       d_vt, packed, g, w.plan, w.comp3, status, grid, w.aent, w.splitlist,
-                       w.splitcount, w.gk, sg);
+    ApproxSeg as{nullptr, 0, w.aent, w.degen, w.plan, w.splitlist, w.irrseg, status};
+    if (segp) {   // the segment products in their own slot (WS_VAGG), a fresh tag per call
+        if (!agg) return hipErrorInvalidValue;
+        as.agg = agg;
+        as.epoch = lookback_epoch();
+    }
+    hipLaunchKernelGGL(k_vit_approx, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, d_vt,
+                       w.comp1, as);
+    if (!segp)
+        hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks + head), dim3(kScanT), 0, s, vc,
+                           packed, g, w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount,
+                           w.vhead);
+    const size_t nbz = (size_t)(vc.emax - vc.emin + 1);
+    const size_t lds3x = (nbz * 16 * 2 + std::max(nbz * 64 * 2, (size_t)kW4 * 2)) * sizeof(double2);
+    // K3 + K3b in one launch: the chunks' irregular blocks run as extra workgroups (segment
+    // path: and block 0's walks, one lane per chunk)
+    const unsigned heads3 = segp ? (unsigned)((nchunks + kThreads - 1) / kThreads) : 0u;
+    hipLaunchKernelGGL(k_vit_exact, dim3(grid + (unsigned)nchunks + heads3), dim3(kThreads), lds3x,
+                       s, vc, d_vt, packed, g, w.plan, w.comp3, status, grid, w.aent, w.splitlist,
+                       w.splitcount, w.gk, sg, segp ? w.irrseg : nullptr, w.vhead);
     if (segp)
         hipLaunchKernelGGL(k_vit_chain_seg, dim3((unsigned)nchunks), dim3(kSegT), 0, s, vc, packed,
                            g, w.plan, w.comp3, w.degen, w.gk, sg, w.entry, w.went, w.gap,

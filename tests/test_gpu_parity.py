@@ -570,3 +570,33 @@ def test_fused_finalize_across_grid_sizes(gpu_ctx, torch_dev):
         assert np.max(np.abs(e[nz] - ref[nz]) / np.abs(ref[nz])) < ESTEP_RTOL, nch
         c = D.count_labelled(gpu_ctx, dp, ds, n, TRAIN).cpu().numpy()
         assert np.array_equal(c, co.count_labelled(obs[:n], truth[:n], TRAIN)), nch
+
+
+def test_viterbi_islands_calls_of_changing_size(gpu_ctx, torch_dev):
+    """Calls of different chunk counts back to back: the workspace layout changes between
+    them, and the look-back words (Viterbi segment products, island counts) live in slots of
+    their own, so no stale word of another array can pass for this call's tag.  Every chunk
+    decodes as in one call over all chunks (chunks are independent)."""
+    import torch
+    from cpgisland_amd import device as D
+    D1 = 1 << 20
+    nmax = 64
+    packed, _ = D.synth_host(4242, 0, nmax * D1)
+    dp, _ = _dev_genome(packed, np.zeros(nmax * D1 // 32, np.uint32), torch_dev)
+    m = _model(co.initial_model())
+    so_all, sc_all = D.viterbi(gpu_ctx, m, dp, nmax * D1, D1)
+    out_all, c_all = D.islands(gpu_ctx, dp, so_all, nmax * D1, D1)
+    torch.cuda.synchronize()
+    gpu_ctx.sync()
+    ref = so_all.cpu().numpy().view(np.uint32)
+    isl_all = D.islands_to_numpy(out_all, c_all)
+    for nch in [49, 64, 17, 3, 64, 49, 1, 33]:
+        so, sc = D.viterbi(gpu_ctx, m, dp, nch * D1, D1)
+        out, c = D.islands(gpu_ctx, dp, so, nch * D1, D1)
+        torch.cuda.synchronize()
+        gpu_ctx.sync()
+        w = nch * D1 // 32
+        assert np.array_equal(so.cpu().numpy().view(np.uint32)[:w], ref[:w]), nch
+        assert np.array_equal(sc.cpu().numpy()[:nch], sc_all.cpu().numpy()[:nch]), nch
+        isl = D.islands_to_numpy(out, c)
+        assert np.array_equal(isl, isl_all[isl_all["chunk"] < nch]), nch
