@@ -163,8 +163,8 @@ def _cpu_model():
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=400)
+    ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--bases", type=int, default=N_PER_GPU, help="bases per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--separate-train", action="store_true",

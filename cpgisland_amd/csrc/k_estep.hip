@@ -303,8 +303,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     auto* bins = reinterpret_cast<unsigned long long*>(TA4);  // [64 rows][16 columns]
     auto* part = reinterpret_cast<unsigned long long*>(
         smem + kUnionOff + kUnionBytes);
-    double4* fck4 = reinterpret_cast<double4*>(part + 16 * 64);   // [NMB-1][nl] products
-    double2* fck = reinterpret_cast<double2*>(fck4);              // then the checkpoints
+    double2* fck = reinterpret_cast<double2*>(part + 16 * 64);   // [NMB][nl] alpha checkpoints
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int64_t c = blockIdx.x;
@@ -362,9 +361,12 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     // 1. lane product of M_p over its positions: per mini-block, its four 4-step matrices
     //    multiplied as a tree (W0 W1)(W2 W3), then into the running product (position 0
     //    carries no matrix: lane 0's first window is M_1 M_2 M_3).  The running products
-    //    after mini-blocks 0 .. NMB-2 (the alpha checkpoints' factors) go to LDS ([m][lane]
-    //    x 32 B; the exponent is dropped: alpha's scale per position is free).
+    //    after mini-blocks 0 .. NMB-2 (the alpha checkpoints' factors) stay in registers
+    //    through the scans (the exponent is dropped: alpha's scale per position is free) —
+    //    in LDS they took 96 KB, which kept the decode kernels' workgroups (K3: ~37 KB) off
+    //    the training CUs.
     Mat P = mid();
+    double4 Pk[NMB - 1];
 #pragma unroll
     for (int g = 0; g < NMB; ++g) {
         double2 ra[4], rb[4];
@@ -395,7 +397,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         const Mat G{w01.a * w23.a + w01.b * w23.c, w01.a * w23.b + w01.b * w23.d,
                     w01.c * w23.a + w01.d * w23.c, w01.c * w23.b + w01.d * w23.d, 0};
         P = mmul(P, G);   // normalised
-        if (g < NMB - 1) fck4[g * nl + t] = make_double4(P.a, P.b, P.c, P.d);
+        if (g < NMB - 1) Pk[g] = make_double4(P.a, P.b, P.c, P.d);
     }
     CPG_EST_MARK(T2)
     // 2. prefix and suffix products of the lane products: shuffle scans inside each wave
@@ -476,17 +478,17 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     }
     vnorm(bP, bM);
     CPG_EST_MARK(T3)
-    // the alpha checkpoints (see 3a) of mini-blocks 1.. in LDS ([m-1][lane], the first 16 B
-    // of each 32-B product slot: conflict-free rows); mini-block 0's, (aP, aM) itself, in the
-    // second half of slot [0][lane] (no register stays live across the main loop for it)
+    // the alpha checkpoints (see 3a) of every mini-block in LDS ([m][lane], 16 B: a wave's
+    // row is conflict-free per 8-lane pass); mini-block 0's is (aP, aM) itself (no register
+    // stays live across the main loop for it)
 #pragma unroll
     for (int m = 1; m < NMB; ++m) {
-        const double4 A = fck4[(m - 1) * nl + t];
+        const double4 A = Pk[m - 1];
         double xP = aP * A.x + aM * A.z, xM = aP * A.y + aM * A.w;
         vnorm(xP, xM);
-        fck[2 * ((m - 1) * nl + t)] = make_double2(xP, xM);
+        fck[m * nl + t] = make_double2(xP, xM);
     }
-    fck[2 * t + 1] = make_double2(aP, aM);
+    fck[t] = make_double2(aP, aM);
     __syncthreads();
     CPG_EST_MARK(T4)
 
@@ -514,7 +516,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         const uint32_t pw = (t > 0 || m > 0) ? pk[4 * t + m - 1] : 0u;
         const uint64_t cm = codes16(xw, pw >> 30);
         // alpha at the position before the mini-block (its checkpoint)
-        const double2 f = fck[m > 0 ? 2 * ((m - 1) * nl + t) : 2 * t + 1];
+        const double2 f = fck[m * nl + t];
         const double bfP = f.x, bfM = f.y;
         // alpha registers hold one half of the mini-block: the second half's alphas from a
         // forward pass over all 16 positions, then (after its backward pass) the first half's
@@ -762,9 +764,12 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
 size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep + 1024; }
 
 namespace {
+#ifndef CPG_EST_LDS_PAD
+#define CPG_EST_LDS_PAD 0   // measurement only: extra LDS per workgroup (co-residency probe)
+#endif
 size_t estep_lds(int lanes) {   // the union is sized for 16 waves; fewer lanes use a prefix
     return kUnionOff + kUnionBytes + 16 * 64 * sizeof(unsigned long long) +
-           (size_t)(kLanePos / 16 - 1) * lanes * sizeof(double4);
+           (size_t)(kLanePos / 16) * lanes * sizeof(double2) + CPG_EST_LDS_PAD;
 }
 }  // namespace
 
