@@ -86,6 +86,13 @@ __device__ __forceinline__ Mat mmul(const Mat& x, const Mat& y) {
     mnorm(r);
     return r;
 }
+// product without the renormalisation: inside a scan of normalised positive products the
+// entries of two or three unnormalised levels stay far inside fp64's range, so the scans
+// renormalise only at their last level (a normalisation is ~11 VALU of the ~20 of a product)
+__device__ __forceinline__ Mat mmul_nn(const Mat& x, const Mat& y) {
+    return {x.a * y.a + x.b * y.c, x.a * y.b + x.b * y.d, x.c * y.a + x.d * y.c,
+            x.c * y.b + x.d * y.d, x.e + y.e};
+}
 __device__ __forceinline__ Mat mid() { return {1.0, 0.0, 0.0, 1.0, 0}; }
 __device__ __forceinline__ Mat msel(bool c, const Mat& x, const Mat& y) {   // field selects
     return {c ? x.a : y.a, c ? x.b : y.b, c ? x.c : y.c, c ? x.d : y.d, c ? x.e : y.e};
@@ -407,8 +414,8 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1) {   // inside rows: DPP (identity at row edges)
         const Mat yp = row_up(xp, off), ys = row_down(xs, off);
-        xp = mmul(yp, xp);
-        xs = mmul(xs, ys);
+        xp = off < 8 ? mmul_nn(yp, xp) : mmul(yp, xp);
+        xs = off < 8 ? mmul_nn(xs, ys) : mmul(xs, ys);
     }
     // across rows (the LDS crossbar), the row totals: prefix — rows 1, 3 take the last lane
     // of the row before, then rows 2, 3 take lane 31; suffix — rows 0, 2 take the first lane
@@ -416,7 +423,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     {
         const int row = lane >> 4;
         Mat yp = shfl_mat(xp, (lane | 15) - 16), ys = shfl_mat(xs, (lane & ~15) + 16);
-        Mat np = mmul(yp, xp), ns = mmul(xs, ys);
+        Mat np = mmul_nn(yp, xp), ns = mmul_nn(xs, ys);
         xp = msel(row & 1, np, xp);
         xs = msel(!(row & 1), ns, xs);
         yp = shfl_mat(xp, 31);
@@ -441,8 +448,8 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
 #pragma unroll
         for (int off = 1; off < 16; off <<= 1) {   // the 16 wave totals: row 0, DPP
             const Mat yp = row_up(wp, off), ys = row_down(ws, off);
-            wp = mmul(yp, wp);
-            ws = mmul(ws, ys);
+            wp = off < 8 ? mmul_nn(yp, wp) : mmul(yp, wp);
+            ws = off < 8 ? mmul_nn(ws, ys) : mmul(ws, ys);
         }
         const Mat ep = row_up(wp, 1), es = row_down(ws, 1);
         if (t < nw) {
