@@ -16,8 +16,11 @@ namespace cpg {
 int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
     Buf& b = ctx->ws[slot];
     if (b.bytes < bytes) {
+        // the whole device, not only the context's stream: calls run on callers' streams
+        // (torch streams, the streamed genome's non-blocking streams), and a kernel still
+        // reading the old buffer there must finish before it is freed
         if (b.p) {
-            CPG_HIP(hipStreamSynchronize(ctx->stream));
+            CPG_HIP(hipDeviceSynchronize());
             CPG_HIP(hipFree(b.p));
             b.p = nullptr;
             b.bytes = 0;
@@ -25,8 +28,10 @@ int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
         size_t sz = bytes + bytes / 8 + 4096;
         CPG_HIP(hipMalloc(&b.p, sz));
         // zero-filled once: the count / E-step accumulators rely on it (their final kernels
-        // re-zero them after reading)
+        // re-zero them after reading); the fill is on the null stream, which non-blocking
+        // streams do not wait for: wait for it here
         CPG_HIP(hipMemset(b.p, 0, sz));
+        CPG_HIP(hipDeviceSynchronize());
         b.bytes = sz;
     }
     *out = b.p;
