@@ -254,7 +254,17 @@ def main():
     icap = 1 << 20
 
     def make_lane(cx):
-        return {"ctx": cx,
+        # the training pass writes one rank record per step (E-step doubles | labelled-count
+        # int64: cpgisland_amd/dist.py train_record), double-buffered so that step k+1's
+        # training pass does not wait for step k's all-gather
+        recs = [cdist.train_record(dev) for _ in range(2)]
+        return {"ctx": cx, "recs": recs,
+                "gath": [torch.empty(world * cdist.TRAIN_RECORD, dtype=torch.float64, device=dev)
+                         for _ in range(2)],
+                "ev_tr": [torch.cuda.Event() for _ in range(2)],
+                "ev_red": [torch.cuda.Event() for _ in range(2)],
+                "emerged": torch.empty(105, dtype=torch.float64, device=dev),
+                "lmerged": torch.empty(124, dtype=torch.int64, device=dev),
                 "so": torch.empty(D.words32(N) + 4, dtype=torch.int32, device=dev),
                 "score": torch.empty(max(ndec, 1), dtype=torch.float64, device=dev),
                 "ecnt": torch.empty(105, dtype=torch.float64, device=dev),
@@ -322,6 +332,9 @@ def main():
         # the decode stream at high priority: its latency-bound kernels get CUs first as the
         # E-step's workgroups retire, the E-step fills the rest
         ln["s_dec"] = main_s if args.serial else torch.cuda.Stream(priority=-1 if args.prio else 0)
+        # the reducer's collective on a stream of its own: the next step's training pass does
+        # not wait for it
+        ln["s_red"] = main_s if args.serial else torch.cuda.Stream()
 
     def step(it, k):
         ln = lanes[k % nlanes]
@@ -366,27 +379,36 @@ def main():
                           count=part["icnt"] if part else ln["icnt"])
                 if pi == 0:
                     mark("islands", 1)
+        par = k & 1
+        rec, ecnt, lcnt = ln["recs"][par]
         with torch.cuda.stream(s_tr):
+            if dist and k >= 2:   # this record's previous all-gather has read it
+                s_tr.wait_event(ln["ev_red"][par])
             if fused:   # "estep" = the whole training pass (E-step + labelled counts)
                 mark("estep", 0)
-                D.train_pass(cx, model0, dp, ds, N, TRAIN, estep_out=ln["ecnt"],
-                             counts_out=ln["lcnt"])
+                D.train_pass(cx, model0, dp, ds, N, TRAIN, estep_out=ecnt, counts_out=lcnt)
                 mark("estep", 1)
             else:
                 mark("estep", 0)
-                D.bw_estep(cx, model0, dp, N, TRAIN, out=ln["ecnt"])
+                D.bw_estep(cx, model0, dp, N, TRAIN, out=ecnt)
                 mark("estep", 1)
                 mark("counts", 0)
-                D.count_labelled(cx, dp, ds, N, TRAIN, out=ln["lcnt"])
+                D.count_labelled(cx, dp, ds, N, TRAIN, out=lcnt)
                 mark("counts", 1)
-            mark("reduce", 0)
-            if dist:   # the reducer: int64 sums are exact in any order; fp64 in rank order
-                cdist.merge_counts_i64(ln["lcnt"])
-                cdist.merge_counts_f64(ln["ecnt"])
-            mark("reduce", 1)
+            if dist:
+                ln["ev_tr"][par].record(s_tr)
+        if dist:   # the reducer over ranks: one all-gather of the records + one merge launch
+            with torch.cuda.stream(ln["s_red"]):
+                ln["s_red"].wait_event(ln["ev_tr"][par])
+                mark("reduce", 0)
+                cdist.merge_train_records(cx, rec, ln["emerged"], ln["lmerged"],
+                                          gathered=ln["gath"][par])
+                mark("reduce", 1)
+                ln["ev_red"][par].record(ln["s_red"])
         if args.no_overlap or args.serial:
             main_s.wait_stream(s_tr)
             main_s.wait_stream(s_dec)
+            main_s.wait_stream(ln["s_red"])
 
     for w in range(args.warmup):
         step(None, w)
@@ -407,6 +429,7 @@ def main():
     for ln in lanes:
         main_s.wait_stream(ln["s_tr"])
         main_s.wait_stream(ln["s_dec"])
+        main_s.wait_stream(ln["s_red"])
         for part in ln["parts"]:
             main_s.wait_stream(part["s"])
     torch.cuda.synchronize()

@@ -403,6 +403,16 @@ int cpg_train_pass_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_pac
     return CPG_OK;
 }
 
+int cpg_merge_train_d(cpg_ctx* ctx, const void* d_gathered, int world, double* d_estep,
+                      int64_t* d_counts, void* stream) {
+    if (!ctx || !d_gathered || !d_estep || !d_counts || world < 1)
+        return set_error(CPG_E_INVALID, "cpg_merge_train_d: bad argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    CPG_HIP(launch_merge_train(d_gathered, world, d_estep, d_counts, pick(ctx, stream)));
+    return CPG_OK;
+}
+
 int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compat_quirks,
                  uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result,
                  void* stream) {

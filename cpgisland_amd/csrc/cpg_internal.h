@@ -195,6 +195,9 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
                         int64_t chunk_len, unsigned long long* acc, double* out,
                         hipStream_t s, int parts = PART_ALL, const double2* gtab = nullptr);
 size_t estep_ws_bytes(int64_t nchunks, int64_t chunk_len);
+// the reducer over ranks: gathered records -> summed outputs (k_reduce.hip)
+hipError_t launch_merge_train(const void* gathered, int world, double* estep, int64_t* counts,
+                              hipStream_t s);
 // the fused training pass (E-step + labelled counts in one launch; k_estep.hip)
 bool train_fusable(int64_t chunk_len);
 hipError_t launch_train(const cpg_model& model, const uint32_t* packed, const uint32_t* sign,

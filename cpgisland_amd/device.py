@@ -97,6 +97,15 @@ def train_pass(ctx: Context, model: HmmModel, packed: torch.Tensor, sign: torch.
     return estep_out, counts_out
 
 
+def merge_train(ctx: Context, gathered: torch.Tensor, world: int, estep_out: torch.Tensor,
+                counts_out: torch.Tensor):
+    """cpg_merge_train_d: `world` gathered rank records (TRAIN_RECORD words each: the E-step
+    doubles, then the labelled-count int64) -> the fp64 sums in rank order + the int64 sums."""
+    check(lib.cpg_merge_train_d(ctx.handle, _dp(gathered), world, _dp(estep_out),
+                                _dp(counts_out), _stream()))
+    return estep_out, counts_out
+
+
 def viterbi(ctx: Context, model: HmmModel, packed: torch.Tensor, nbases: int,
             chunk_len: int = _lib.DECODE_CHUNK, sign_out: torch.Tensor | None = None,
             score: torch.Tensor | None = None):

@@ -84,6 +84,45 @@ def merge_counts_f64(counts: torch.Tensor, group=None) -> torch.Tensor:
     return counts
 
 
+TRAIN_RECORD = 105 + 124   # words: cpg_counts_f64 doubles, then cpg_counts_i64 int64
+
+
+def train_record(device):
+    """One rank's training-pass record (CPG_TRAIN_RECORD_BYTES): a float64 tensor whose first
+    105 words are the E-step counts and whose last 124 are the labelled counts (int64 view)
+    — pass the two views to device.train_pass as its outputs."""
+    rec = torch.empty(TRAIN_RECORD, dtype=torch.float64, device=device)
+    return rec, rec[:105], rec[105:].view(torch.int64)
+
+
+def merge_train_records(ctx, rec: torch.Tensor, estep_out: torch.Tensor, counts_out: torch.Tensor,
+                        group=None, gathered: torch.Tensor | None = None):
+    """The reducer over ranks in one collective: all-gather of every rank's record, then every
+    rank sums the records itself (cpg_merge_train_d on the GPU: doubles in rank order —
+    bitwise identical on every rank — and exact integers; numpy on CPU tensors)."""
+    ws = _group_size(group)
+    if gathered is None:
+        gathered = torch.empty(ws * TRAIN_RECORD, dtype=torch.float64, device=rec.device)
+    if ws > 1:
+        if dist.get_backend(group) == "nccl":
+            dist.all_gather_into_tensor(gathered, rec, group=group)
+        else:
+            dist.all_gather(list(gathered.view(ws, TRAIN_RECORD)), rec, group=group)
+    else:
+        gathered.copy_(rec)
+    if rec.is_cuda:
+        from . import device as D
+        D.merge_train(ctx, gathered, ws, estep_out, counts_out)
+    else:
+        g = gathered.view(ws, TRAIN_RECORD)
+        e = g[0, :105].clone()
+        for r in range(1, ws):
+            e += g[r, :105]
+        estep_out.copy_(e)
+        counts_out.copy_(g[:, 105:].contiguous().view(torch.int64).sum(dim=0))
+    return estep_out, counts_out
+
+
 def gather_islands(records: np.ndarray, device, group=None) -> np.ndarray:
     """Concatenate every rank's island records (ISLAND_DTYPE) in rank order, on all ranks."""
     ws = _group_size(group)

@@ -189,6 +189,16 @@ int cpg_train_pass_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_pac
                      const uint32_t* d_sign, int64_t nbases, int64_t chunk_len,
                      double* d_estep_counts, int64_t* d_label_counts, void* stream);
 
+/* The reducer over ranks (:200-203, multi-GPU): d_gathered holds `world` rank records, each
+ * CPG_COUNTS_F64_N doubles (the rank's cpg_counts_f64) followed by CPG_COUNTS_I64_N int64
+ * (its cpg_counts_i64) — CPG_TRAIN_RECORD_BYTES bytes, e.g. the output of one all-gather of
+ * every rank's record.  d_estep (CPG_COUNTS_F64_N doubles) = the fp64 records summed in rank
+ * order (bitwise identical on every rank), d_counts (CPG_COUNTS_I64_N int64) = the exact
+ * integer sums.  One launch. */
+#define CPG_TRAIN_RECORD_BYTES ((CPG_COUNTS_F64_N + CPG_COUNTS_I64_N) * 8)
+int cpg_merge_train_d(cpg_ctx* ctx, const void* d_gathered, int world, double* d_estep,
+                      int64_t* d_counts, void* stream);
+
 /* Viterbi decode, HmmEvaluator.decode(trainedModel, chunk, true) (:260), of every
  * whole chunk_len chunk (tail not decoded, :256).  Output: the state path as sign bits
  * (state = base + (sign ? 0 : 4)), identical to Mahout's sequential fp64 Viterbi, and

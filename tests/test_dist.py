@@ -52,6 +52,14 @@ def _worker(rank, world, port, q):
         # E-step counts: all-gather + rank-order sum (identical bits on every rank)
         part = co.estep(m, o, TRAIN)
         fe = cd.merge_counts_f64(torch.from_numpy(part.copy()))
+        # the same reduction as one all-gather of each rank's training record (bench.py's
+        # reducer): identical bits
+        rec, re, rc = cd.train_record("cpu")
+        re.copy_(torch.from_numpy(part))
+        rc.copy_(torch.from_numpy(co.count_labelled(o, tr, TRAIN)))
+        me, mc = torch.empty(105, dtype=torch.float64), torch.empty(124, dtype=torch.int64)
+        cd.merge_train_records(None, rec, me, mc)
+        assert torch.equal(me, fe) and torch.equal(mc, li)
         # decode: per shard, global chunk numbering, gathered in genome order
         recs = [co.islands(co.viterbi8(m, o[c * DECODE:(c + 1) * DECODE])[0],
                            start // DECODE + c) for c in range(n // DECODE)]

@@ -600,3 +600,31 @@ def test_viterbi_islands_calls_of_changing_size(gpu_ctx, torch_dev):
         assert np.array_equal(sc.cpu().numpy()[:nch], sc_all.cpu().numpy()[:nch]), nch
         isl = D.islands_to_numpy(out, c)
         assert np.array_equal(isl, isl_all[isl_all["chunk"] < nch]), nch
+
+
+@pytest.mark.parametrize("world", [1, 2, 8])
+def test_merge_train_records(gpu_ctx, torch_dev, world):
+    """cpg_merge_train_d (the reducer over ranks): the fp64 parts summed in rank order —
+    bitwise the sequential sum — and the int64 parts exactly, from one gathered buffer."""
+    import torch
+    from cpgisland_amd import device as D
+    from cpgisland_amd import dist as cd
+    rng = np.random.default_rng(world)
+    e = rng.random((world, 105)) * 10.0 ** rng.integers(-3, 9, (world, 105))
+    c = rng.integers(0, 1 << 40, (world, 124), dtype=np.int64)
+    g = np.concatenate([e, c.view(np.float64)], axis=1).reshape(-1)
+    gd = torch.from_numpy(g.copy()).to(torch_dev)
+    oe = torch.empty(105, dtype=torch.float64, device=torch_dev)
+    oc = torch.empty(124, dtype=torch.int64, device=torch_dev)
+    D.merge_train(gpu_ctx, gd, world, oe, oc)
+    ref = e[0].copy()
+    for r in range(1, world):
+        ref += e[r]
+    assert np.array_equal(oe.cpu().numpy(), ref)
+    assert np.array_equal(oc.cpu().numpy(), c.sum(axis=0))
+    # the single-process record path (world 1 without a process group) is the identity
+    rec, re_, rc = cd.train_record(torch_dev)
+    re_.copy_(torch.from_numpy(e[0]))
+    rc.copy_(torch.from_numpy(c[0]))
+    cd.merge_train_records(gpu_ctx, rec, oe, oc)
+    assert np.array_equal(oe.cpu().numpy(), e[0]) and np.array_equal(oc.cpu().numpy(), c[0])
