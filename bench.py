@@ -167,6 +167,10 @@ def main():
     ap.add_argument("--warmup", type=int, default=20)
     ap.add_argument("--bases", type=int, default=N_PER_GPU, help="bases per GPU")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--probe-sleep", type=str, default="",
+                    help="measurement probe: STREAM:CYCLES adds a one-thread spin kernel "
+                         "(torch.cuda._sleep) per step on the decode ('dec') or training ('tr') "
+                         "stream, to price a stream's latency")
     ap.add_argument("--separate-train", action="store_true",
                     help="E-step and labelled counts as two launches instead of the fused "
                          "training pass (cpg_train_pass_d)")
@@ -291,6 +295,10 @@ def main():
     # point of record): 10 per step cost ~9 % of the overlapped throughput, 4 per step ~3 %,
     # the E-step's 2 per step plus the decode's on every 4th step ~1 %.
     full_ev = args.phase_events or args.serial
+    probe = None
+    if args.probe_sleep:
+        ps_, pc_ = args.probe_sleep.split(":")
+        probe = (ps_, int(pc_))
     fused = not args.separate_train
     names = ("estep", "counts", "reduce", "viterbi", "islands") if full_ev else ("estep", "decode")
     # one pair of HIP events per phase per timed step, read after the final synchronize (no
@@ -379,6 +387,8 @@ def main():
                           count=part["icnt"] if part else ln["icnt"])
                 if pi == 0:
                     mark("islands", 1)
+                    if probe and probe[0] == "dec":
+                        torch.cuda._sleep(probe[1])
         par = k & 1
         rec, ecnt, lcnt = ln["recs"][par]
         with torch.cuda.stream(s_tr):
@@ -395,6 +405,8 @@ def main():
                 mark("counts", 0)
                 D.count_labelled(cx, dp, ds, N, TRAIN, out=lcnt)
                 mark("counts", 1)
+            if probe and probe[0] == "tr":
+                torch.cuda._sleep(probe[1])
             if dist:
                 ln["ev_tr"][par].record(s_tr)
         if dist:   # the reducer over ranks: one all-gather of the records + one merge launch
