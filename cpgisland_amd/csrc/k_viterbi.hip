@@ -585,13 +585,14 @@ __device__ void approx_segment(const VitConsts& vc, const Geo& g, const uint32_t
         const unsigned long long t0 = wall_clock64();
         unsigned long long f;
         for (;;) {
-            f = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(f >> 32) == as.epoch) break;
+            // deadline first: a limit of 0 gives up deterministically (the test hook)
             if (wall_clock64() - t0 >= (unsigned long long)(CPG_VIT_SPIN_LIMIT)) {
                 atomicOr(as.status, ST_VIT_LOOKBACK);
                 f = 0;
                 break;
             }
+            f = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if ((uint32_t)(f >> 32) == as.epoch) break;
             __builtin_amdgcn_s_sleep(1);
         }
         sPre[t] = f;

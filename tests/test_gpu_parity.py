@@ -628,3 +628,42 @@ def test_merge_train_records(gpu_ctx, torch_dev, world):
     rc.copy_(torch.from_numpy(c[0]))
     cd.merge_train_records(gpu_ctx, rec, oe, oc)
     assert np.array_equal(oe.cpu().numpy(), e[0]) and np.array_equal(oc.cpu().numpy(), c[0])
+
+
+def test_viterbi_lookback_timeout_is_an_error(gpu_ctx):
+    """The Viterbi segment path's look-back over a chunk's earlier segments (K1) is a bounded
+    spin; in libcpg_isl_timeout.so the bound is 0 (CPG_VIT_SPIN_LIMIT=0), so every segment
+    after a chunk's first gives up: the call fails with CPG_E_DEVICE (ST_VIT_LOOKBACK) instead
+    of returning a path.  Chunks of one segment (64 Ki) have no look-back and still decode."""
+    import ctypes as C
+    import os
+    from cpgisland_amd import _lib
+    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libcpg_isl_timeout.so")
+    assert os.path.exists(path), "build it: make -C cpgisland_amd/csrc"
+    lib = C.CDLL(path)
+    lib.cpg_open.argtypes = [C.c_int, C.c_void_p]
+    lib.cpg_close.argtypes = [C.c_void_p]
+    lib.cpg_last_error.restype = C.c_char_p
+    lib.cpg_viterbi.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                C.c_void_p, C.c_void_p]
+    n = 2 << 20
+    packed, _ = __import__("cpgisland_amd.device", fromlist=["synth_host"]).synth_host(5, 0, n)
+    packed = np.ascontiguousarray(packed.astype(np.uint32))
+    m = np.ascontiguousarray(co.initial_model())
+    sign = np.zeros(n // 32 + 4, np.uint32)
+    score = np.zeros(64, np.float64)
+    ctx = C.c_void_p()
+    assert lib.cpg_open(0, C.byref(ctx)) == 0
+    try:
+        rc = lib.cpg_viterbi(ctx, m.ctypes.data, packed.ctypes.data, n, 1 << 20,
+                             sign.ctypes.data, score.ctypes.data)
+        assert rc == _lib.CPG_E_DEVICE, rc
+        assert b"look-back" in lib.cpg_last_error()
+        rc1 = lib.cpg_viterbi(ctx, m.ctypes.data, packed.ctypes.data, n, 65536,
+                              sign.ctypes.data, score.ctypes.data)
+        assert rc1 == 0
+        st, best = co.viterbi8(m, pr.unpack(packed, 65536))
+        assert np.array_equal(pr.unpack_bits(sign, 65536), (st < 4).astype(np.uint8))
+        assert score[0] == best
+    finally:
+        lib.cpg_close(ctx)
