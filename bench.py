@@ -123,8 +123,22 @@ def train_step(ctx, model0, dp, ds, N, ecnt, lcnt, fused):
         D.count_labelled(ctx, dp, ds, N, TRAIN, out=lcnt)
 
 
+def decode_step(ctx, model1, dp, N, so, score, iout, icnt, fused, first_chunk=0):
+    """The decode: Viterbi + island scan of the same chunks — one call (cpg_decode_d: the
+    traceback writes the island scan's run records) or the two single calls
+    (--separate-decode)."""
+    from cpgisland_amd import device as D
+    if fused:
+        D.decode(ctx, model1, dp, N, DECODE, cap=iout.shape[0], first_chunk=first_chunk,
+                 sign_out=so, score=score, out=iout, count=icnt)
+    else:
+        D.viterbi(ctx, model1, dp, N, DECODE, sign_out=so, score=score)
+        D.islands(ctx, dp, so, N, DECODE, cap=iout.shape[0], first_chunk=first_chunk, out=iout,
+                  count=icnt)
+
+
 def cold_cache_steps(ln, dp, ds, N, model0, model1, nsteps, main_s, dev, flush_mb=1024,
-                     fused=True):
+                     fused=True, fused_decode=True):
     """The step on one stream, each behind a 1 GiB scratch write that evicts the shard from
     the 256 MB Infinity Cache; HIP events bracket the step's kernels only (not the flush)."""
     from cpgisland_amd import device as D
@@ -136,9 +150,8 @@ def cold_cache_steps(ln, dp, ds, N, model0, model1, nsteps, main_s, dev, flush_m
             a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
             a.record()
             train_step(ln["ctx"], model0, dp, ds, N, ln["ecnt"], ln["lcnt"], fused)
-            D.viterbi(ln["ctx"], model1, dp, N, DECODE, sign_out=ln["so"], score=ln["score"])
-            D.islands(ln["ctx"], dp, ln["so"], N, DECODE, cap=ln["iout"].shape[0],
-                      out=ln["iout"], count=ln["icnt"])
+            decode_step(ln["ctx"], model1, dp, N, ln["so"], ln["score"], ln["iout"], ln["icnt"],
+                        fused_decode)
             b.record()
             pairs.append((a, b))
     torch.cuda.synchronize()
@@ -171,6 +184,9 @@ def main():
                     help="measurement probe: STREAM:CYCLES adds a one-thread spin kernel "
                          "(torch.cuda._sleep) per step on the decode ('dec') or training ('tr') "
                          "stream, to price a stream's latency")
+    ap.add_argument("--separate-decode", action="store_true",
+                    help="Viterbi and island scan as two calls instead of the fused decode "
+                         "(cpg_decode_d)")
     ap.add_argument("--separate-train", action="store_true",
                     help="E-step and labelled counts as two launches instead of the fused "
                          "training pass (cpg_train_pass_d)")
@@ -300,7 +316,10 @@ def main():
         ps_, pc_ = args.probe_sleep.split(":")
         probe = (ps_, int(pc_))
     fused = not args.separate_train
-    names = ("estep", "counts", "reduce", "viterbi", "islands") if full_ev else ("estep", "decode")
+    fused_decode = not args.separate_decode
+    names = (("estep", "counts", "reduce") +
+             (("decode",) if fused_decode else ("viterbi", "islands"))) if full_ev \
+        else ("estep", "decode")
     # one pair of HIP events per phase per timed step, read after the final synchronize (no
     # host round trip between steps)
     evs = [{k: (torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
@@ -359,6 +378,8 @@ def main():
                 key = name
             elif (name, i) in (("viterbi", 0), ("islands", 1)) and it % args.decode_event_every == 0:
                 key, i = "decode", (0 if name == "viterbi" else 1)
+            elif name == "decode" and it % args.decode_event_every == 0:
+                key = "decode"
             else:
                 return
             evs[it][key][i].record()
@@ -375,18 +396,27 @@ def main():
             part = ln["parts"][pi - 1] if pi > 0 else None
             with torch.cuda.stream(part["s"] if part else s_dec):
                 px = part["ctx"] if part else cx
-                if pi == 0:
-                    mark("viterbi", 0)
                 pp, sg = dp[c0 * DECODE // 16:], ln["so"][c0 * DECODE // 32:]
-                D.viterbi(px, model1, pp, nb, DECODE, sign_out=sg, score=ln["score"][c0:])
-                if pi == 0:
-                    mark("viterbi", 1)
-                    mark("islands", 0)
-                D.islands(px, pp, sg, nb, DECODE, cap=icap, first_chunk=first_chunk + c0,
-                          out=part["iout"] if part else ln["iout"],
-                          count=part["icnt"] if part else ln["icnt"])
-                if pi == 0:
-                    mark("islands", 1)
+                io = part["iout"] if part else ln["iout"]
+                ic = part["icnt"] if part else ln["icnt"]
+                if fused_decode:
+                    if pi == 0:
+                        mark("decode", 0)
+                    D.decode(px, model1, pp, nb, DECODE, cap=icap, first_chunk=first_chunk + c0,
+                             sign_out=sg, score=ln["score"][c0:], out=io, count=ic)
+                    if pi == 0:
+                        mark("decode", 1)
+                else:
+                    if pi == 0:
+                        mark("viterbi", 0)
+                    D.viterbi(px, model1, pp, nb, DECODE, sign_out=sg, score=ln["score"][c0:])
+                    if pi == 0:
+                        mark("viterbi", 1)
+                        mark("islands", 0)
+                    D.islands(px, pp, sg, nb, DECODE, cap=icap, first_chunk=first_chunk + c0,
+                              out=io, count=ic)
+                    if pi == 0:
+                        mark("islands", 1)
                     if probe and probe[0] == "dec":
                         torch.cuda._sleep(probe[1])
         par = k & 1
@@ -464,7 +494,7 @@ def main():
     cold = None
     if args.cold_steps > 0 and not dist and not args.flush_mb:
         cold = cold_cache_steps(lanes[0], dp, ds, N, model0, model1, args.cold_steps, main_s, dev,
-                                fused=fused)
+                                fused=fused, fused_decode=fused_decode)
     steps = args.steps
     ms_per_step = elapsed * 1e3 / steps
     value = N * world * steps / elapsed
@@ -505,7 +535,7 @@ def main():
                      "achieved": round(fl, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(fl / FP64_PEAK_TFLOPS, 4),
                      "flops_per_base": ESTEP_FLOPS_PER_BASE}
-        vit = phases["viterbi"] + phases["islands"] if full_ev else phases["decode"]
+        vit = phases["decode"] if "decode" in phases else phases["viterbi"] + phases["islands"]
         roof_decode = {"phase": "viterbi+islands", "achieved": round(
             (BYTES_PER_BASE["viterbi"] + BYTES_PER_BASE["islands"]) * N / (vit / 1e3) / 1e9
             if vit > 0 else 0.0, 1),
@@ -521,6 +551,8 @@ def main():
                           "streams": 1 if args.serial else 2,
                           "train_pass": ("fused: cpg_train_pass_d, E-step + labelled counts in "
                                          "one launch" if fused else "separate launches"),
+                          "decode": ("fused: cpg_decode_d, traceback writes the island run "
+                                     "records" if fused_decode else "separate calls"),
                           "decode_priority": "high" if (args.prio and not args.serial) else "normal",
                           "step_overlap": not (args.no_overlap or args.serial),
                           "pipeline_lanes": nlanes,

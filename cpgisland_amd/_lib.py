@@ -73,6 +73,7 @@ SIGNATURES = {
     "cpg_viterbi_d": [_P, _P, _P, _I64, _I64, _P, _P, _P],
     "cpg_islands_d": [_P, _P, _P, _I64, _I64, _P, _I64, _P, _P],
     "cpg_islands_at_d": [_P, _P, _P, _I64, _I64, _I64, _P, _I64, _P, _P],
+    "cpg_decode_d": [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _I64, _P, _P],
     "cpg_count_labelled": [_P, _P, _P, _I64, _I64, _P],
     "cpg_bw_estep": [_P, _P, _P, _I64, _I64, _P],
     "cpg_viterbi": [_P, _P, _P, _I64, _I64, _P, _P],

@@ -10,6 +10,7 @@
 #include <atomic>
 
 #include "cpg_internal.h"
+#include "isl_dev.h"
 
 namespace cpg {
 
@@ -203,6 +204,7 @@ int cpg_reserve(cpg_ctx* ctx, int64_t nbases) {
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
     if ((rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
     if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nd + 1) * 8, &p))) return rc;
+    if ((rc = ws_get(ctx, WS_IDONE, (size_t)(nd + 1) * 4, &p))) return rc;
     if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nt, CPG_TRAIN_CHUNK), &p))) return rc;
     return CPG_OK;
 }
@@ -347,6 +349,66 @@ int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_s
     CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, first_chunk, ws,
                            ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status,
                            pick(ctx, stream), static_cast<unsigned long long*>(fl)));
+    return CPG_OK;
+}
+
+int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                 int64_t nbases, int64_t chunk_len, int64_t first_chunk, uint32_t* d_sign_out,
+                 double* d_score, cpg_island* d_out, int64_t cap, int64_t* d_count,
+                 void* stream) {
+    if (!ctx || !model || !d_sign_out || !d_count || (cap > 0 && !d_out))
+        return set_error(CPG_E_INVALID, "null argument");
+    int rc = check_layout(d_packed, nbases, chunk_len);
+    if (rc) return rc;
+    const int64_t nch = nbases / chunk_len;
+    if (nch > 1 && chunk_len % 256)
+        return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 256 for >1 chunk");
+    if (chunk_len % 32) return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 32");
+    if (!aligned16(d_sign_out)) return set_error(CPG_E_INVALID, "sign_out not 16-byte aligned");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    hipStream_t s = pick(ctx, stream);
+    const int64_t w_done = (nch * chunk_len + 31) / 32, w_all = (nbases + 31) / 32;
+    const int64_t ntail = w_all > w_done ? w_all - w_done : 0;
+    void* wsi;
+    if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &wsi))) return rc;
+    void* fl;
+    if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nch + 1) * 8, &fl))) return rc;
+    if (nch == 0) {
+        if (ntail) CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)ntail * 4, s));
+        CPG_HIP(hipMemsetAsync(d_count, 0, sizeof(int64_t), s));
+        return CPG_OK;
+    }
+    VitConsts vc;
+    static thread_local VitTables vt;
+    if ((rc = vit_prepare(model, chunk_len, &vc, &vt))) return rc;
+    const VitTables* d_vt;
+    if ((rc = vit_tables(ctx, model, vc, vt, &d_vt))) return rc;
+    void* ws;
+    if ((rc = ws_get(ctx, WS_VIT, viterbi_ws_bytes(nch, chunk_len), &ws))) return rc;
+    void* agg;
+    if ((rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(nch, chunk_len), &agg))) return rc;
+    // fused: the traceback writes the island run records and a chunk's last traceback
+    // workgroup resolves it — no island kernels
+    if (islands_fusable(nch, chunk_len)) {
+        void* done;
+        if ((rc = ws_get(ctx, WS_IDONE, (size_t)nch * 4, &done))) return rc;
+        IslFuse fz;
+        CPG_HIP(islands_fuse(&fz, wsi, ctx->ws[WS_ISL].bytes, nch, chunk_len, first_chunk, d_out,
+                             cap, d_count, ctx->d_status, static_cast<unsigned long long*>(fl),
+                             static_cast<unsigned int*>(done)));
+        CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
+                               d_sign_out, d_score, nullptr, ctx->d_status, s,
+                               static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,
+                               &fz));
+        return CPG_OK;
+    }
+    CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
+                           d_sign_out, d_score, nullptr, ctx->d_status, s,
+                           static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail));
+    CPG_HIP(launch_islands(d_packed, d_sign_out, nch, chunk_len, first_chunk, wsi,
+                           ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status, s,
+                           static_cast<unsigned long long*>(fl)));
     return CPG_OK;
 }
 

@@ -37,6 +37,8 @@ enum : uint32_t {
 
 // ---- Viterbi constants (host-computed, shared by every kernel) ---------------------
 constexpr int kMaxBinade = 64;
+struct IslFuse;   // a fused decode's island state (isl_dev.h)
+
 struct VitConsts {
     double L[16][4];        // per dinucleotide d = p | b<<2: log a for +->+, -->+, +->-, -->-
     double logpi[8];
@@ -118,7 +120,10 @@ enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5,
        // look-back words tagged with a per-call epoch (Viterbi segment products, island
        // counts): slots of their own, so that stale words are only older tags — never other
        // arrays of a differently laid-out earlier call whose bits could pass for the tag
-       WS_VAGG = 16, WS_IFLG = 17, WS_NSLOT = 18 };
+       WS_VAGG = 16, WS_IFLG = 17,
+       // per-chunk done counters of the fused decode: zero between calls (zero-filled when
+       // allocated, reset by the workgroup that completes a chunk), so a slot of their own
+       WS_IDONE = 18, WS_NSLOT = 19 };
 // a fresh look-back tag per call: an odd multiple of a counter (a bijection: distinct for 2^32
 // calls), never 0 (zero-filled workspace) or all ones
 uint32_t lookback_epoch();
@@ -177,7 +182,8 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                           int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
                           uint32_t* sign_out, double* score, uint8_t* degen,
                           uint32_t* status, hipStream_t s, unsigned long long* agg,
-                          uint32_t* zero_at = nullptr, int64_t zero_n = 0);
+                          uint32_t* zero_at = nullptr, int64_t zero_n = 0,
+                          const IslFuse* fuse = nullptr);   // fused decode: K7 resolves
 size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len);
 size_t viterbi_agg_bytes(int64_t nchunks, int64_t chunk_len);   // WS_VAGG
 // model-derived LDS tables of K1/K3, built once per model right after the VitTables copy
@@ -190,6 +196,13 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
                           hipStream_t s, unsigned long long* flags,
                           const int64_t* base_in = nullptr);   // flags: WS_IFLG, nchunks words
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
+// fused decode (cpg_decode_d): the traceback writes the island tile lists and a chunk's last
+// traceback workgroup resolves it (no island kernels); done: WS_IDONE, nchunks words
+bool islands_fusable(int64_t nchunks, int64_t chunk_len);
+hipError_t islands_fuse(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
+                        int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
+                        int64_t* count, uint32_t* status, unsigned long long* flags,
+                        unsigned int* done, const int64_t* base_in = nullptr);
 // gtab: the model's one-step tables in device memory (est_tables); needed with PART_ACC
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t chunk_len, unsigned long long* acc, double* out,

@@ -43,6 +43,7 @@
 #include <cmath>
 
 #include "cpg_internal.h"
+#include "isl_dev.h"
 
 namespace cpg {
 namespace {
@@ -1883,16 +1884,89 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
 }
 
 // ---------------------------------------------------------------- K7: traceback
+
+// Fused decode (cpg_decode_d): the workgroup is one island tile (its 256 blocks, inside one
+// chunk).  From the block's 8 sign words just traced, its 16 packed words, the packed word
+// and the state before the block, every lane counts its words (C, G, CpG, run starts and
+// closes: isl_dev.h), one workgroup scan gives the tile-relative prefix at each word, and
+// lanes holding a run boundary write its records — the island tile kernel's work without
+// reading the sign words back.  Records and totals are agent-scope atomic stores: the
+// chunk's last workgroup reads them (k_vit_trace).
+__device__ __forceinline__ void trace_tile(const uint32_t (&out)[8], const uint32_t (&P)[16],
+                                           uint32_t pprev, uint32_t sprev, int64_t k,
+                                           const isl::IslWs& tl) {
+    using namespace isl;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    Cnt5 n{0, 0, 0, 0, 0};
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+        n = cadd(n, cnt_of(masks_reg(out[i], i ? out[i - 1] : sprev, P[2 * i], P[2 * i + 1],
+                                     i ? P[2 * i - 1] : pprev)));
+    // a wave's sums fit 16 bits (<= 64 x 256): two fields per word
+    const uint32_t own0 = (uint32_t)n.c | ((uint32_t)n.g << 16),
+                   own1 = (uint32_t)n.cg | ((uint32_t)n.st << 16), own2 = (uint32_t)n.cl;
+    uint32_t x0 = own0, x1 = own1, x2 = own2;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y0 = __shfl_up(x0, off), y1 = __shfl_up(x1, off), y2 = __shfl_up(x2, off);
+        if (lane >= off) {
+            x0 += y0;
+            x1 += y1;
+            x2 += y2;
+        }
+    }
+    __shared__ Cnt5 wt[kThreads / 64];
+    if (lane == 63)
+        wt[wv] = Cnt5{(int32_t)(x0 & 0xFFFFu), (int32_t)(x0 >> 16), (int32_t)(x1 & 0xFFFFu),
+                      (int32_t)(x1 >> 16), (int32_t)x2};
+    __syncthreads();
+    Cnt5 e{0, 0, 0, 0, 0}, tot{0, 0, 0, 0, 0};
+#pragma unroll
+    for (int w = 0; w < kThreads / 64; ++w) {
+        const Cnt5 v = wt[w];
+        if (w < wv) e = cadd(e, v);
+        tot = cadd(tot, v);
+    }
+    const uint32_t ex0 = x0 - own0, ex1 = x1 - own1, ex2 = x2 - own2;
+    e = cadd(e, Cnt5{(int32_t)(ex0 & 0xFFFFu), (int32_t)(ex0 >> 16), (int32_t)(ex1 & 0xFFFFu),
+                     (int32_t)(ex1 >> 16), (int32_t)ex2});
+    if (n.st | n.cl) {   // the lane's words hold a run boundary
+        RunRec* st = tl.starts + (int64_t)blockIdx.x * tl.cap_t;
+        RunRec* cl = tl.closes + (int64_t)blockIdx.x * tl.cap_t;
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            emit_word<true>(masks_reg(out[i], i ? out[i - 1] : sprev, P[2 * i], P[2 * i + 1],
+                                i ? P[2 * i - 1] : pprev),
+                      k * 8 + i, e, st, cl);
+    }
+    if (t == 0) st_cnt5<true>(tl.ttot + blockIdx.x, tot);
+}
+
+template <bool kIsl>
 __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __restrict__ bp,
                                                         const uint8_t* __restrict__ endst,
                                                         uint32_t* __restrict__ sign_out,
                                                         uint32_t* status, uint32_t* zero_at,
-                                                        int64_t zero_n) {
+                                                        int64_t zero_n,
+                                                        const uint32_t* __restrict__ packed,
+                                                        IslFuse fz) {
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     // the undecoded tail's sign words ('-'), in this launch rather than a memset of its own
     for (int64_t i = gid; i < zero_n; i += (int64_t)gridDim.x * kThreads) zero_at[i] = 0u;
+    // kIsl: the grid is whole workgroups of whole blocks (no lane leaves before the barrier)
     if (gid >= g.nchunks * g.nsb) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
+    uint32_t P[16], pprev = 0u;
+    if constexpr (kIsl) {   // the block's 256 bases: issued first, used after the traceback
+        const uint32_t* pk = packed + c * (g.C >> 4) + k * 16;
+        const uint4* p4 = reinterpret_cast<const uint4*>(pk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const uint4 v = p4[i];
+            P[4 * i] = v.x; P[4 * i + 1] = v.y; P[4 * i + 2] = v.z; P[4 * i + 3] = v.w;
+        }
+        if (k > 0) pprev = pk[-1];
+    }
     uint32_t wP[8], wM[8];
     {
         const int64_t nt = g.nchunks * g.nsb;   // quad-major layout (k_vit_forward)
@@ -1931,7 +2005,8 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
     }
     // block 0: bit 0 of out[0] is the state of position 0 itself; otherwise the state
     // reached before the block must be the previous block's end state
-    if (k > 0 && s != endst[gid - 1]) atomicOr(status, ST_VERIFY_CHAIN);
+    const uint32_t sb = k > 0 ? endst[gid - 1] : 0u;   // the state before the block
+    if (k > 0 && s != sb) atomicOr(status, ST_VERIFY_CHAIN);
     // write the block's words (positions k*256 ... k*256+255 of the chunk)
     uint32_t* so = sign_out + c * (g.C >> 5) + k * 8;
     const int64_t nw = (g.C + 31) >> 5;
@@ -1943,6 +2018,27 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
 #pragma unroll
         for (int w = 0; w < 8; ++w)
             if (k * 8 + w < nw) so[w] = out[w];
+    }
+    if constexpr (kIsl) {
+        trace_tile(out, P, pprev, sb << 31, k, fz.ws);
+        // the chunk's last workgroup to finish resolves it (its records are complete): the
+        // island resolve kernel's work, overlapped with the other chunks' tracebacks
+        __shared__ int s_last;
+        __builtin_amdgcn_s_waitcnt(0);   // this wave's record stores have completed
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const unsigned wpc = (unsigned)(g.nsb / kThreads);
+            const unsigned old = __hip_atomic_fetch_add(fz.done + c, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            s_last = old == wpc - 1;
+            if (s_last)   // zero again for the next call
+                __hip_atomic_store(fz.done + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (!s_last) return;
+        __shared__ isl::ResolveLds L;
+        __shared__ isl::Cnt5 s_to[kThreads / 16];
+        isl::resolve_chunk<true, kThreads / 16>(packed, g.C, fz.ws, fz.o, c, L, s_to);
     }
 }
 
@@ -2020,7 +2116,7 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                           int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
                           uint32_t* sign_out, double* score, uint8_t* degen_out,
                           uint32_t* status, hipStream_t s, unsigned long long* agg,
-                          uint32_t* zero_at, int64_t zero_n) {
+                          uint32_t* zero_at, int64_t zero_n, const IslFuse* fuse) {
     const int64_t nsb = vit_nsb(chunk_len);
     VitWs w = carve(ws, nchunks, nsb);
     if (w.bytes > ws_bytes) return hipErrorInvalidValue;
@@ -2068,8 +2164,15 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                        w.entry, w.bp, w.origin, status, w.gk, sg, w.went);
     hipLaunchKernelGGL(k_vit_tscan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, g, w.entry,
                        w.origin, w.endst, score);
-    hipLaunchKernelGGL(k_vit_trace, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst, sign_out,
-                       status, zero_at, zero_n);
+    if (fuse) {   // fused decode: the workgroups are whole island tiles inside one chunk
+        if (nsb % kThreads || chunk_len != nsb * kSB || fuse->ws.ntile != nsb / kThreads)
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_vit_trace<true>, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst,
+                           sign_out, status, zero_at, zero_n, packed, *fuse);
+    } else {
+        hipLaunchKernelGGL(k_vit_trace<false>, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst,
+                           sign_out, status, zero_at, zero_n, nullptr, IslFuse{});
+    }
     if (degen_out) {
         hipError_t e = hipMemcpyAsync(degen_out, w.degen, nchunks, hipMemcpyDeviceToDevice, s);
         if (e != hipSuccess) return e;

@@ -134,6 +134,28 @@ def islands(ctx: Context, packed: torch.Tensor, sign: torch.Tensor, nbases: int,
     return out, count
 
 
+def decode(ctx: Context, model: HmmModel, packed: torch.Tensor, nbases: int,
+           chunk_len: int = _lib.DECODE_CHUNK, cap: int = 1 << 20, first_chunk: int = 0,
+           sign_out: torch.Tensor | None = None, score: torch.Tensor | None = None,
+           out: torch.Tensor | None = None, count: torch.Tensor | None = None):
+    """viterbi() then islands() in one call (cpg_decode_d): the reference's decode loop body
+    (CpGIslandFinder.java:260 then :262-339).  Returns (sign_out, score, out, count)."""
+    nch = nbases // chunk_len
+    dev = packed.device
+    if sign_out is None:
+        sign_out = torch.empty(words32(nbases) + 4, dtype=torch.int32, device=dev)
+    if score is None:
+        score = torch.empty(max(nch, 1), dtype=torch.float64, device=dev)
+    if out is None:
+        out = torch.empty((max(cap, 1), _lib.ISLAND_DTYPE.itemsize), dtype=torch.uint8, device=dev)
+    if count is None:
+        count = torch.zeros(1, dtype=torch.int64, device=dev)
+    m = model.to_struct()
+    check(lib.cpg_decode_d(ctx.handle, ptr(m), _dp(packed), nbases, chunk_len, first_chunk,
+                           _dp(sign_out), _dp(score), _dp(out), cap, _dp(count), _stream()))
+    return sign_out, score, out, count
+
+
 def islands_to_numpy(out: torch.Tensor, count: torch.Tensor) -> np.ndarray:
     n = int(count.item())
     n = min(n, out.shape[0])

@@ -222,6 +222,18 @@ int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_s
                      int64_t nbases, int64_t chunk_len, int64_t first_chunk,
                      cpg_island* d_out, int64_t cap, int64_t* d_count, void* stream);
 
+/* The reference's decode loop body in one call: HmmEvaluator.decode (:260) then the island
+ * scan + filter (:262-339) of every whole chunk — cpg_viterbi_d followed by
+ * cpg_islands_at_d(first_chunk) on the same buffers, with identical outputs (d_sign_out,
+ * d_score, d_out, *d_count).  When chunk_len is a multiple of 65,536 (the reference's
+ * 1 Mi decode chunk) the traceback kernel also writes the island scan's run records from
+ * the sign words it produces, so the sign bits are not read back.  Contracts: as the two
+ * calls. */
+int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                 int64_t nbases, int64_t chunk_len, int64_t first_chunk, uint32_t* d_sign_out,
+                 double* d_score, cpg_island* d_out, int64_t cap, int64_t* d_count,
+                 void* stream);
+
 /* Device-side ASCII ingest: the reference's readers (CpGIslandFinder.java:112-145, mode 0 =
  * training; :238-259, mode 1 = decode) over raw text already in HBM, with exactly the
  * semantics of cpg_ingest (same quirks, same committed prefix, same error rules).  d_txt:

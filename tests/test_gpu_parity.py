@@ -600,6 +600,91 @@ def test_viterbi_islands_calls_of_changing_size(gpu_ctx, torch_dev):
         assert np.array_equal(sc.cpu().numpy()[:nch], sc_all.cpu().numpy()[:nch]), nch
         isl = D.islands_to_numpy(out, c)
         assert np.array_equal(isl, isl_all[isl_all["chunk"] < nch]), nch
+        # the fused decode (per-chunk done counters reused across calls of other sizes)
+        so2, sc2, out2, c2 = D.decode(gpu_ctx, m, dp, nch * D1, D1)
+        torch.cuda.synchronize()
+        gpu_ctx.sync()
+        assert np.array_equal(so2.cpu().numpy().view(np.uint32)[:w], ref[:w]), nch
+        assert np.array_equal(sc2.cpu().numpy()[:nch], sc_all.cpu().numpy()[:nch]), nch
+        assert np.array_equal(D.islands_to_numpy(out2, c2), isl), nch
+
+
+def _switchy_model(scale):
+    """The reference's initial model with the +/- switches made `scale` times likelier:
+    Viterbi paths of many short runs (island records across every tile border)."""
+    pi, a, b = co.model_split(co.initial_model())
+    a2 = a.copy()
+    a2[:4, 4:] *= scale
+    a2[4:, :4] *= scale
+    a2 /= a2.sum(axis=1, keepdims=True)
+    return co.model_flat(pi, a2, b)
+
+
+@pytest.mark.parametrize("C,nch", [(1 << 16, 5), (1 << 20, 3), (1 << 17, 2), (1 << 21, 2),
+                                   (1 << 15, 4), (4096, 9)])
+@pytest.mark.parametrize("model", ["initial", "switchy"])
+def test_decode_fused_vs_oracle_and_separate_calls(gpu_ctx, torch_dev, C, nch, model):
+    """cpg_decode_d (Viterbi + islands in one call; for chunk lengths that are multiples of
+    65,536 the traceback writes the island run records itself) against the oracle's decode
+    loop (:256-340: states, best scores, island records) and bitwise against the two single
+    calls, with a chunk offset (first_chunk) and a tail past the last whole chunk."""
+    import torch
+    from cpgisland_amd import device as D
+    N = nch * C + 777
+    packed, _ = D.synth_host(900 + C % 97, 0, N)
+    obs = pr.unpack(packed, N)
+    m = co.initial_model() if model == "initial" else _switchy_model(40.0)
+    dp, _ = _dev_genome(packed, np.zeros(N // 32 + 1, np.uint32), torch_dev)
+    hm = _model(m)
+    so, sc, out, cnt = D.decode(gpu_ctx, hm, dp, N, C, cap=1 << 18)
+    torch.cuda.synchronize()
+    gpu_ctx.sync()
+    states, isl_ref, score = co.decode_chunks(m, obs, C)
+    nd = len(states)
+    sg = D.sign_to_numpy(so, N)
+    assert np.array_equal(sg[:nd], (states < 4).astype(np.uint8))
+    assert not sg[nd:].any()
+    assert np.array_equal(sc.cpu().numpy()[:nch], score)
+    got = D.islands_to_numpy(out, cnt)
+    assert np.array_equal(got, isl_ref)
+    if model == "switchy":
+        assert len(isl_ref) > 8 * nch * C // 65536, len(isl_ref)
+    # bitwise the two single calls, chunk numbering from 7
+    so2, sc2, out2, cnt2 = D.decode(gpu_ctx, hm, dp, N, C, cap=1 << 18, first_chunk=7)
+    so3, sc3 = D.viterbi(gpu_ctx, hm, dp, N, C)
+    out3, cnt3 = D.islands(gpu_ctx, dp, so3, N, C, cap=1 << 18, first_chunk=7)
+    torch.cuda.synchronize()
+    gpu_ctx.sync()
+    w = (N + 31) // 32
+    assert np.array_equal(so2.cpu().numpy()[:w], so3.cpu().numpy()[:w])
+    assert np.array_equal(sc2.cpu().numpy()[:nch], sc3.cpu().numpy()[:nch])
+    assert np.array_equal(D.islands_to_numpy(out2, cnt2), D.islands_to_numpy(out3, cnt3))
+    assert np.array_equal(D.islands_to_numpy(out2, cnt2)["chunk"], got["chunk"] + 7)
+
+
+def test_decode_fused_capacity_and_empty(gpu_ctx, torch_dev):
+    """cpg_decode_d: *d_count is the full count when records exceed cap (first cap records
+    written), and a call with no whole chunk writes count 0 and a '-' tail."""
+    import torch
+    from cpgisland_amd import device as D
+    C = 1 << 16
+    N = 4 * C
+    packed, _ = D.synth_host(77, 0, N)
+    dp, _ = _dev_genome(packed, np.zeros(N // 32 + 1, np.uint32), torch_dev)
+    hm = _model(_switchy_model(40.0))
+    _, _, out, cnt = D.decode(gpu_ctx, hm, dp, N, C, cap=1 << 16)
+    _, _, out3, cnt3 = D.decode(gpu_ctx, hm, dp, N, C, cap=3)
+    torch.cuda.synchronize()
+    gpu_ctx.sync()
+    full = D.islands_to_numpy(out, cnt)
+    assert int(cnt3.item()) == len(full) > 3
+    assert np.array_equal(out3[:3].cpu().numpy().reshape(-1).view(co.ISLAND_DTYPE), full[:3])
+    so = torch.full((8,), -1, dtype=torch.int32, device=torch_dev)
+    _, _, _, c0 = D.decode(gpu_ctx, hm, dp, 100, C, sign_out=so)
+    torch.cuda.synchronize()
+    gpu_ctx.sync()
+    assert int(c0.item()) == 0
+    assert so.cpu().numpy()[:4].tolist() == [0, 0, 0, 0]
 
 
 @pytest.mark.parametrize("world", [1, 2, 8])
