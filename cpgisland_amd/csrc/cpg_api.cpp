@@ -204,7 +204,7 @@ int cpg_reserve(cpg_ctx* ctx, int64_t nbases) {
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
     if ((rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
     if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nd + 1) * 8, &p))) return rc;
-    if ((rc = ws_get(ctx, WS_IDONE, (size_t)(nd + 1) * 4, &p))) return rc;
+    if ((rc = ws_get(ctx, WS_IDONE, (size_t)(nd + 1) * 8, &p))) return rc;
     if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nt, CPG_TRAIN_CHUNK), &p))) return rc;
     return CPG_OK;
 }
@@ -306,9 +306,12 @@ int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed
     if ((rc = ws_get(ctx, WS_VIT, need, &ws))) return rc;
     void* agg;
     if ((rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(nch, chunk_len), &agg))) return rc;
+    void* done;   // per-chunk counters: K5's workgroups, then (cpg_decode_d) K7's
+    if ((rc = ws_get(ctx, WS_IDONE, (size_t)nch * 8, &done))) return rc;
     CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
                            d_sign_out, d_score, nullptr, ctx->d_status, s,
-                           static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail));
+                           static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,
+                           nullptr, static_cast<unsigned int*>(done)));
     return CPG_OK;
 }
 
@@ -388,24 +391,26 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
     if ((rc = ws_get(ctx, WS_VIT, viterbi_ws_bytes(nch, chunk_len), &ws))) return rc;
     void* agg;
     if ((rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(nch, chunk_len), &agg))) return rc;
+    void* dn;   // per-chunk counters: K5's workgroups [0, nch), K7's [nch, 2 nch)
+    if ((rc = ws_get(ctx, WS_IDONE, (size_t)nch * 8, &dn))) return rc;
+    unsigned int* done = static_cast<unsigned int*>(dn);
     // fused: the traceback writes the island run records and a chunk's last traceback
     // workgroup resolves it — no island kernels
     if (islands_fusable(nch, chunk_len)) {
-        void* done;
-        if ((rc = ws_get(ctx, WS_IDONE, (size_t)nch * 4, &done))) return rc;
         IslFuse fz;
         CPG_HIP(islands_fuse(&fz, wsi, ctx->ws[WS_ISL].bytes, nch, chunk_len, first_chunk, d_out,
                              cap, d_count, ctx->d_status, static_cast<unsigned long long*>(fl),
-                             static_cast<unsigned int*>(done)));
+                             done + nch));
         CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
                                d_sign_out, d_score, nullptr, ctx->d_status, s,
                                static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,
-                               &fz));
+                               &fz, done));
         return CPG_OK;
     }
     CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
                            d_sign_out, d_score, nullptr, ctx->d_status, s,
-                           static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail));
+                           static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,
+                           nullptr, done));
     CPG_HIP(launch_islands(d_packed, d_sign_out, nch, chunk_len, first_chunk, wsi,
                            ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status, s,
                            static_cast<unsigned long long*>(fl)));

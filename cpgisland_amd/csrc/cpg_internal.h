@@ -183,7 +183,8 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                           uint32_t* sign_out, double* score, uint8_t* degen,
                           uint32_t* status, hipStream_t s, unsigned long long* agg,
                           uint32_t* zero_at = nullptr, int64_t zero_n = 0,
-                          const IslFuse* fuse = nullptr);   // fused decode: K7 resolves
+                          const IslFuse* fuse = nullptr,    // fused decode: K7 resolves
+                          unsigned int* done5 = nullptr);   // nchunks zeroed words: K5 runs K6
 size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len);
 size_t viterbi_agg_bytes(int64_t nchunks, int64_t chunk_len);   // WS_VAGG
 // model-derived LDS tables of K1/K3, built once per model right after the VitTables copy
@@ -197,7 +198,7 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
                           const int64_t* base_in = nullptr);   // flags: WS_IFLG, nchunks words
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
 // fused decode (cpg_decode_d): the traceback writes the island tile lists and a chunk's last
-// traceback workgroup resolves it (no island kernels); done: WS_IDONE, nchunks words
+// traceback workgroup resolves it (no island kernels); done: nchunks zeroed words (WS_IDONE)
 bool islands_fusable(int64_t nchunks, int64_t chunk_len);
 hipError_t islands_fuse(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
                         int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,

@@ -1659,29 +1659,16 @@ __device__ __forceinline__ uint32_t quad_origin(uint64_t hP, uint64_t hM) {
     return (uint32_t)((~hM & 1u) | ((~hP & 1u) << 1));
 }
 
-__global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const uint32_t* packed,
-                                                          Geo g, const uint8_t* __restrict__ degen,
-                                                          const double2* __restrict__ entry,
-                                                          uint4* __restrict__ bp,
-                                                          uint8_t* __restrict__ origin,
-                                                          uint32_t* status,
-                                                          const double4* __restrict__ rx,
-                                                          const SegSum* __restrict__ seg,
-                                                          const double2* __restrict__ went) {
-    // conflict-free halves (16 x 16 B each); entry 16 is the identity step (0, -inf, -inf,
-    // 0) standing for block 0's position 0: P + 0.0 = P and M + -inf = -inf exactly, so the
-    // values, the tie bits that matter and the origins are unchanged by it
-    __shared__ double2 LA[17], LB[17];
-    if (threadIdx.x < 16) {
-        LA[threadIdx.x] = make_double2(vc.L[threadIdx.x][0], vc.L[threadIdx.x][1]);
-        LB[threadIdx.x] = make_double2(vc.L[threadIdx.x][2], vc.L[threadIdx.x][3]);
-    } else if (threadIdx.x == 16) {
-        LA[16] = make_double2(0.0, -INFINITY);
-        LB[16] = make_double2(-INFINITY, 0.0);
-    }
-    __syncthreads();
-    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
-    if (gid >= g.nchunks * g.nsb) return;
+// one block's re-forward (lane = block gid): backpointers, the self-check; returns the
+// block's origin map
+__device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_t* packed,
+                                              const Geo& g, const uint8_t* __restrict__ degen,
+                                              const double2* __restrict__ entry,
+                                              uint4* __restrict__ bp, uint32_t* status,
+                                              const double4* __restrict__ rx,
+                                              const SegSum* __restrict__ seg,
+                                              const double2* __restrict__ went,
+                                              const double2* LA, const double2* LB, int64_t gid) {
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     // backpointers quad-major: bp[q * nt + gid] = {bP bits 0-31, 32-63, bM bits 0-31, 32-63} of
     // the block's quad q (64 steps), so that each quad's store is one coalesced 16-B/lane row
@@ -1689,8 +1676,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
     uint4* bpo = bp + gid;
     if (degen[c]) {
         for (int i = 0; i < 4; ++i) bpo[i * nt] = make_uint4(0, 0, 0, 0);
-        origin[gid] = 0x2;   // identity
-        return;
+        return 0x2u;   // identity
     }
     const uint32_t* pk = chunk_ptr(packed, g, c);
     const double2* ent = entry + c * (g.nsb + 1);
@@ -1811,20 +1797,38 @@ __global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const ui
             }
         }
     }
-    origin[gid] = (uint8_t)(oM | (oP << 1));
     const double2 nx = vnext;
     if (__double_as_longlong(nx.x) != __double_as_longlong(P) ||
         __double_as_longlong(nx.y) != __double_as_longlong(M))
         atomicOr(status, ST_VERIFY_ENTRY);
+    return oM | (oP << 1);
 }
 
 // ---------------------------------------------------------------- K6: trace scan
 
-__global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __restrict__ entry,
-                                                        const uint8_t* __restrict__ origin,
-                                                        uint8_t* __restrict__ endst,
-                                                        double* __restrict__ score) {
-    const int64_t c = blockIdx.x;
+// origin maps written by an earlier kernel (plain loads) or by other workgroups of this one
+// (K5's chunk tail: agent-scope atomic words, see k_vit_forward)
+template <bool kAgent>
+__device__ __forceinline__ uint32_t ld_org4(const uint8_t* p) {   // 4 maps, p 4-B aligned
+    if constexpr (kAgent)
+        return __hip_atomic_load(reinterpret_cast<const uint32_t*>(p), __ATOMIC_RELAXED,
+                                 __HIP_MEMORY_SCOPE_AGENT);
+    else
+        return *reinterpret_cast<const uint32_t*>(p);
+}
+template <bool kAgent>
+__device__ __forceinline__ uint32_t ld_org(const uint8_t* og, int64_t k) {
+    if constexpr (kAgent) return (ld_org4<true>(og + (k & ~3ll)) >> (8 * (k & 3))) & 0xFFu;
+    else return og[k];
+}
+
+// K6's work for chunk c (one workgroup of kThreads lanes): final argmax, suffix scan of the
+// block origin maps, every block's end state
+template <bool kAgent>
+__device__ __forceinline__ void tscan_chunk(const Geo& g, const double2* __restrict__ entry,
+                                            const uint8_t* __restrict__ origin,
+                                            uint8_t* __restrict__ endst,
+                                            double* __restrict__ score, int64_t c) {
     const int t = threadIdx.x;
     const int64_t per = (g.nsb + kThreads - 1) / kThreads;
     const int64_t b0 = t * per, b1 = min(b0 + per, g.nsb);
@@ -1837,8 +1841,13 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
     const bool vec = per == 16 && g.nsb % 16 == 0, have = b0 < b1;
     uint32_t ow[4] = {0, 0, 0, 0};
     if (vec && have) {
-        const uint4 w = *reinterpret_cast<const uint4*>(og + b0);
-        ow[0] = w.x; ow[1] = w.y; ow[2] = w.z; ow[3] = w.w;
+        if constexpr (kAgent) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) ow[i] = ld_org4<true>(og + b0 + 4 * i);
+        } else {
+            const uint4 w = *reinterpret_cast<const uint4*>(og + b0);
+            ow[0] = w.x; ow[1] = w.y; ow[2] = w.z; ow[3] = w.w;
+        }
     }
     uint32_t F = 0x2u;
     if (vec) {
@@ -1847,7 +1856,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
             for (int i = 0; i < 16; ++i) F = map_compose(F, (ow[i >> 2] >> (8 * (i & 3))) & 0xFFu);
         }
     } else {
-        for (int64_t k = b0; k < b1; ++k) F = map_compose(F, og[k]);
+        for (int64_t k = b0; k < b1; ++k) F = map_compose(F, ld_org<kAgent>(og, k));
     }
     // suffix composition over the lanes: wave shuffles (down), then the wave totals
     const int lane = t & 63, wv = t >> 6;
@@ -1878,8 +1887,73 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
     } else {
         for (int64_t k = b1 - 1; k >= b0; --k) {
             endst[c * g.nsb + k] = (uint8_t)e;
-            e = map_apply(og[k], e);
+            e = map_apply(ld_org<kAgent>(og, k), e);
         }
+    }
+}
+
+__global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __restrict__ entry,
+                                                        const uint8_t* __restrict__ origin,
+                                                        uint8_t* __restrict__ endst,
+                                                        double* __restrict__ score) {
+    tscan_chunk<false>(g, entry, origin, endst, score, blockIdx.x);
+}
+
+// K5.  kScan (chunks of whole workgroups, nsb % 256 == 0): the chunk's last workgroup to
+// finish also runs K6's scan for it (done: per-chunk counters, zero between calls, reset by
+// that workgroup); the origin maps then cross workgroups inside the kernel, 4 per
+// agent-scope atomic word.
+template <bool kScan>
+__global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const uint32_t* packed,
+                                                          Geo g, const uint8_t* __restrict__ degen,
+                                                          const double2* __restrict__ entry,
+                                                          uint4* __restrict__ bp,
+                                                          uint8_t* __restrict__ origin,
+                                                          uint32_t* status,
+                                                          const double4* __restrict__ rx,
+                                                          const SegSum* __restrict__ seg,
+                                                          const double2* __restrict__ went,
+                                                          unsigned int* done,
+                                                          uint8_t* __restrict__ endst,
+                                                          double* __restrict__ score) {
+    // conflict-free halves (16 x 16 B each); entry 16 is the identity step (0, -inf, -inf,
+    // 0) standing for block 0's position 0: P + 0.0 = P and M + -inf = -inf exactly, so the
+    // values, the tie bits that matter and the origins are unchanged by it
+    __shared__ double2 LA[17], LB[17];
+    if (threadIdx.x < 16) {
+        LA[threadIdx.x] = make_double2(vc.L[threadIdx.x][0], vc.L[threadIdx.x][1]);
+        LB[threadIdx.x] = make_double2(vc.L[threadIdx.x][2], vc.L[threadIdx.x][3]);
+    } else if (threadIdx.x == 16) {
+        LA[16] = make_double2(0.0, -INFINITY);
+        LB[16] = make_double2(-INFINITY, 0.0);
+    }
+    __syncthreads();
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
+    if (gid >= g.nchunks * g.nsb) return;   // (kScan: the grid is whole workgroups)
+    const uint32_t org = fwd_block(vc, packed, g, degen, entry, bp, status, rx, seg, went, LA,
+                                   LB, gid);
+    if constexpr (!kScan) {
+        origin[gid] = (uint8_t)org;
+    } else {
+        const uint32_t o1 = __shfl_down(org, 1), o2 = __shfl_down(org, 2), o3 = __shfl_down(org, 3);
+        if ((threadIdx.x & 3) == 0)
+            __hip_atomic_store(reinterpret_cast<uint32_t*>(origin + gid),
+                               org | (o1 << 8) | (o2 << 16) | (o3 << 24), __ATOMIC_RELAXED,
+                               __HIP_MEMORY_SCOPE_AGENT);
+        __shared__ int s_last;
+        __builtin_amdgcn_s_waitcnt(0);   // this wave's map stores have completed
+        __syncthreads();
+        const int64_t c = gid / g.nsb;
+        if (threadIdx.x == 0) {
+            const unsigned wpc = (unsigned)(g.nsb / kThreads);
+            const unsigned old = __hip_atomic_fetch_add(done + c, 1u, __ATOMIC_RELAXED,
+                                                        __HIP_MEMORY_SCOPE_AGENT);
+            s_last = old == wpc - 1;
+            if (s_last)   // zero again for the next call
+                __hip_atomic_store(done + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+        __syncthreads();
+        if (s_last) tscan_chunk<true>(g, entry, origin, endst, score, c);
     }
 }
 
@@ -2116,7 +2190,8 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                           int64_t nchunks, int64_t chunk_len, void* ws, size_t ws_bytes,
                           uint32_t* sign_out, double* score, uint8_t* degen_out,
                           uint32_t* status, hipStream_t s, unsigned long long* agg,
-                          uint32_t* zero_at, int64_t zero_n, const IslFuse* fuse) {
+                          uint32_t* zero_at, int64_t zero_n, const IslFuse* fuse,
+                          unsigned int* done5) {
     const int64_t nsb = vit_nsb(chunk_len);
     VitWs w = carve(ws, nchunks, nsb);
     if (w.bytes > ws_bytes) return hipErrorInvalidValue;
@@ -2160,10 +2235,18 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
         hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kChainT), 0, s, vc, packed,
                            g, w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout,
                            w.vhead);
-    hipLaunchKernelGGL(k_vit_forward, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.degen,
-                       w.entry, w.bp, w.origin, status, w.gk, sg, w.went);
-    hipLaunchKernelGGL(k_vit_tscan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, g, w.entry,
-                       w.origin, w.endst, score);
+    // chunks of whole K5 workgroups: the trace scan runs in each chunk's last K5 workgroup
+    if (done5 && nsb % kThreads == 0) {
+        hipLaunchKernelGGL(k_vit_forward<true>, dim3(grid), dim3(kThreads), 0, s, vc, packed, g,
+                           w.degen, w.entry, w.bp, w.origin, status, w.gk, sg, w.went, done5,
+                           w.endst, score);
+    } else {
+        hipLaunchKernelGGL(k_vit_forward<false>, dim3(grid), dim3(kThreads), 0, s, vc, packed, g,
+                           w.degen, w.entry, w.bp, w.origin, status, w.gk, sg, w.went, nullptr,
+                           nullptr, nullptr);
+        hipLaunchKernelGGL(k_vit_tscan, dim3((unsigned)nchunks), dim3(kThreads), 0, s, g, w.entry,
+                           w.origin, w.endst, score);
+    }
     if (fuse) {   // fused decode: the workgroups are whole island tiles inside one chunk
         if (nsb % kThreads || chunk_len != nsb * kSB || fuse->ws.ntile != nsb / kThreads)
             return hipErrorInvalidValue;
