@@ -284,6 +284,12 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 // latency-bound waves then fill this kernel's idle issue slots (overlapped bench +3-4 %,
 // tools/ab_libs.sh; a few spills, none of them in the main loop's steady state).  At 4 per
 // SIMD (122 VGPRs, no spills) the kernel alone is as fast; 6 per SIMD spills 38.
+#ifndef EST_BLDS
+#define EST_BLDS 0
+#endif
+#ifndef EST_FPF
+#define EST_FPF 0   // forward table rows (LDS) read this many positions ahead (0: at use)
+#endif
 #ifndef CPG_EST_WPE
 #define CPG_EST_WPE 5
 #endif
@@ -535,11 +541,34 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         int kf[kMB / 4];   // alpha's power-of-two shifts at positions 3, 7, 11, 15
         auto forward = [&](int lo, int hi) {   // positions [0, hi); alphas of [lo, hi) kept
             double xP = bfP, xM = bfM;
+#if EST_FPF
+            // the table rows of position i + EST_FPF issued before position i's products:
+            // the rows depend only on the codes, so the LDS latency leaves the alpha chain
+            double2 fa[EST_FPF + 1], fb[EST_FPF + 1];
+#pragma unroll
+            for (int j = 0; j < EST_FPF; ++j) {
+                const uint32_t d = code_at(cm, j);
+                fa[j] = TA[d];
+                fb[j] = TB[d];
+            }
+#endif
 #pragma unroll
             for (int i = 0; i < hi; ++i) {
+#if EST_FPF
+                if (i + EST_FPF < hi) {
+                    const uint32_t d = code_at(cm, i + EST_FPF);
+                    fa[(i + EST_FPF) % (EST_FPF + 1)] = TA[d];
+                    fb[(i + EST_FPF) % (EST_FPF + 1)] = TB[d];
+                }
+                __builtin_amdgcn_sched_barrier(0);
+#endif
                 if (!(t == 0 && m == 0 && i == 0)) {   // (alpha_0 itself at the chunk start)
+#if EST_FPF
+                    const double2 ma = fa[i % (EST_FPF + 1)], mb = fb[i % (EST_FPF + 1)];
+#else
                     const uint32_t d = code_at(cm, i);
                     const double2 ma = TA[d], mb = TB[d];
+#endif
                     const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
                     xP = nP;
                     xM = nM;
@@ -580,8 +609,13 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
             double2 qa[EST_PFD + 1], qb[EST_PFD + 1];
             auto trow = [&](int i, double2& a, double2& b) {
                 const uint32_t d = code_at(cm, i);
+#if EST_BLDS   // measurement: the rows from the LDS copy (issued ahead of the atomics)
+                a = TA[d];
+                b = TB[d];
+#else
                 a = gtab[d];
                 b = gtab[16 + d];
+#endif
             };
 #pragma unroll
             for (int j = 0; j < EST_PFD; ++j) trow(hi - 1 - j, qa[j], qb[j]);
@@ -612,7 +646,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
                 atomicAdd(wb + bin_of(d, 0) * kBS, raw_fma(uP, t00));
                 atomicAdd(wb + bin_of(d, 1) * kBS, raw_fma(uP, t01));
                 atomicAdd(wb + bin_of(d, 2) * kBS, raw_fma(uM, t10));
+#ifndef EST_DROP4   // measurement only: without the 4th bin's atomic (wrong results)
                 atomicAdd(wb + bin_of(d, 3) * kBS, raw_fma(uM, t11));
+#endif
                 yP = t00 + t01;
                 yM = t10 + t11;
                 if (i == 4 || i == 8 || i == 12) {
