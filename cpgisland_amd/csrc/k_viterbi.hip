@@ -286,6 +286,35 @@ __device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
     return reinterpret_cast<const VitDerived*>(vt + 1);
 }
 
+// Waves per SIMD a kernel is compiled for (VGPR budget 512 / n).  On a training CU the
+// E-step holds 4 waves x 96 VGPRs per SIMD, leaving 128: a decode kernel of <= 64 VGPRs gets
+// two wave slots there instead of one.  K5 (the longest decode kernel under overlap) is built
+// for 8 (64 VGPRs; its few spills are outside the step loop): bench +2 % with the 2-deep
+// lookup ring below (profiles/r02_v10/ab_k5_occupancy*.log).  K3 at 8 (spills) and K7 at 8 (75
+// spills) were slower; K1 cannot reach 64.  The others stay measurement knobs.
+#ifndef VIT_K5_WPE
+#define VIT_K5_WPE 8
+#endif
+#ifdef VIT_K1_WPE
+#define K1_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K1_WPE)))
+#else
+#define K1_ATTR
+#endif
+#ifdef VIT_K3_WPE
+#define K3_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K3_WPE)))
+#else
+#define K3_ATTR
+#endif
+#ifdef VIT_K5_WPE
+#define K5_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K5_WPE)))
+#else
+#define K5_ATTR
+#endif
+#ifdef VIT_K7_WPE
+#define K7_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K7_WPE)))
+#else
+#define K7_ATTR
+#endif
 __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables* vt) {
     VitDerived* dv = reinterpret_cast<VitDerived*>(vt + 1);
     const int n = kQ4 + kMaxBinade * 16 + kMaxBinade * 64 + kMaxBinade * kW4;
@@ -356,7 +385,7 @@ __device__ __forceinline__ int64_t fix_of(double x, int f);
 __device__ __forceinline__ VitPlan classify(const VitConsts& vc, const Geo& g, int64_t k,
                                             longlong2 en, longlong2 ex, bool& irregular);
 
-__global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uint32_t* packed,
+__global__ __launch_bounds__(kThreads) K1_ATTR void k_vit_approx(VitConsts vc, const uint32_t* packed,
                                                          Geo g, const VitTables* vt,
                                                          int4* __restrict__ comp, ApproxSeg as) {
     __shared__ int4 Q[16];
@@ -662,7 +691,7 @@ __device__ __forceinline__ C64 shfl_up_c64(const C64& x, int d) {
     return {__shfl_up(x.pp, d), __shfl_up(x.pm, d), __shfl_up(x.mp, d), __shfl_up(x.mm, d)};
 }
 
-__global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitTables* vt,
+__global__ __launch_bounds__(kThreads) K3_ATTR void k_vit_exact(VitConsts vc, const VitTables* vt,
                                                         const uint32_t* packed, Geo g,
                                                         VitPlan* __restrict__ plan,
                                                         double4* __restrict__ comp3,
@@ -1680,11 +1709,12 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
     }
     const uint32_t* pk = chunk_ptr(packed, g, c);
     const double2* ent = entry + c * (g.nsb + 1);
-    double2 v0, vnext;   // this block's entry, the next block's (the self-check)
-    if (seg) {
-        // segment path (workgroup = segment): entry = anchor value . rx, the anchor being the
-        // last barrier before the block in the segment (K4's value by block id) or, with none,
-        // the segment's entry
+    // segment path (workgroup = segment): a block's entry = anchor value . rx, the anchor
+    // being the last barrier before the block in the segment (K4's value by block id) or,
+    // with none, the segment's entry.  The next block's entry (the self-check) is derived
+    // after the walk, so that nothing of it stays live across the loop.
+    auto entries = [&](bool next) -> double2 {
+        if (!seg) return ent[k + (next ? 1 : 0)];
         const int l = threadIdx.x;
         const SegSum& sg = seg[blockIdx.x];
         const unsigned long long m[4] = {sg.mask[0], sg.mask[1], sg.mask[2], sg.mask[3]};
@@ -1698,17 +1728,14 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
         if (below) a = q * 64 + 63 - (int)__builtin_clzll(below);
         const int64_t sbase = k - l;
         const double2 E = went[blockIdx.x];
-        v0 = c64_apply(a >= 0 ? ent[sbase + a] : E, ld_c64(rx + gid));
+        if (!next) return c64_apply(a >= 0 ? ent[sbase + a] : E, ld_c64(rx + gid));
         if (l + 1 < kThreads) {
             const int a2 = ((mq >> r) & 1ull) ? l : a;
-            vnext = c64_apply(a2 >= 0 ? ent[sbase + a2] : E, ld_c64(rx + gid + 1));
-        } else {
-            vnext = k + 1 == g.nsb ? ent[g.nsb] : went[blockIdx.x + 1];
+            return c64_apply(a2 >= 0 ? ent[sbase + a2] : E, ld_c64(rx + gid + 1));
         }
-    } else {
-        v0 = ent[k];
-        vnext = ent[k + 1];
-    }
+        return k + 1 == g.nsb ? ent[g.nsb] : went[blockIdx.x + 1];
+    };
+    const double2 v0 = entries(false);   // this block's entry
     double P = v0.x, M = v0.y;
     uint32_t oP = 1u, oM = 0u;   // origin sign of the current '+' / '-' survivor
     uint32_t wP0 = 0, wP1 = 0, wM0 = 0, wM1 = 0;
@@ -1734,7 +1761,11 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
     };
     if (g.whole(k)) {
         // quads of 64 steps; the ring of kLook lookups in flight runs across quad borders
-        constexpr int kLook = 4;
+        // (2 deep: at the 64-VGPR budget, 4 had spilled more and measured slower)
+#ifndef VIT_K5_LOOK
+#define VIT_K5_LOOK 2
+#endif
+        constexpr int kLook = VIT_K5_LOOK;
         auto fetch = [&](uint32_t d) { return C64{LA[d].x, LA[d].y, LB[d].x, LB[d].y}; };
         auto code = [](const uint4 w, uint32_t prev, int j) {   // j compile-time, < 64
             const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
@@ -1797,7 +1828,7 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
             }
         }
     }
-    const double2 nx = vnext;
+    const double2 nx = entries(true);   // the next block's entry: the self-check
     if (__double_as_longlong(nx.x) != __double_as_longlong(P) ||
         __double_as_longlong(nx.y) != __double_as_longlong(M))
         atomicOr(status, ST_VERIFY_ENTRY);
@@ -1904,7 +1935,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
 // that workgroup); the origin maps then cross workgroups inside the kernel, 4 per
 // agent-scope atomic word.
 template <bool kScan>
-__global__ __launch_bounds__(kThreads) void k_vit_forward(VitConsts vc, const uint32_t* packed,
+__global__ __launch_bounds__(kThreads) K5_ATTR void k_vit_forward(VitConsts vc, const uint32_t* packed,
                                                           Geo g, const uint8_t* __restrict__ degen,
                                                           const double2* __restrict__ entry,
                                                           uint4* __restrict__ bp,
@@ -2017,7 +2048,7 @@ __device__ __forceinline__ void trace_tile(const uint32_t (&out)[8], const uint3
 }
 
 template <bool kIsl>
-__global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __restrict__ bp,
+__global__ __launch_bounds__(kThreads) K7_ATTR void k_vit_trace(Geo g, const uint4* __restrict__ bp,
                                                         const uint8_t* __restrict__ endst,
                                                         uint32_t* __restrict__ sign_out,
                                                         uint32_t* status, uint32_t* zero_at,
