@@ -295,6 +295,9 @@ __device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
 #ifndef VIT_K5_WPE
 #define VIT_K5_WPE 8
 #endif
+#ifndef VIT_K1_SLIM
+#define VIT_K1_SLIM 0
+#endif
 #ifdef VIT_K1_WPE
 #define K1_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K1_WPE)))
 #else
@@ -392,13 +395,25 @@ __global__ __launch_bounds__(kThreads) K1_ATTR void k_vit_approx(VitConsts vc, c
     // 4-step products over 5-base windows b0..b4 (exact: integers) [0, 1024), then the
     // 3-step products of steps 1..3 over b1..b4 [1024, 1280): block 0's first window (the
     // chunk's position 0 carries no step) — copied from the per-model tables (k_vit_tables)
+#if VIT_K1_SLIM
+    // only the 4-step entries in LDS (16 KB: eight 256-lane
+    // workgroups per CU, so that the compiler may budget 64 VGPRs); block 0's 3-step first
+    // window comes from the global table into the accumulator
+    __shared__ int4 Q4[1024];
+#else
     __shared__ int4 Q4[kQ4];
+#endif
     if (threadIdx.x < 16)
         Q[threadIdx.x] = make_int4(vc.Q[threadIdx.x][0], vc.Q[threadIdx.x][1],
                                    vc.Q[threadIdx.x][2], vc.Q[threadIdx.x][3]);
     const int4* gq = derived(vt)->Q4;
+#if VIT_K1_SLIM
+#pragma unroll
+    for (int i = 0; i < 1024 / kThreads; ++i) Q4[threadIdx.x + i * kThreads] = gq[threadIdx.x + i * kThreads];
+#else
 #pragma unroll
     for (int i = 0; i < kQ4 / kThreads; ++i) Q4[threadIdx.x + i * kThreads] = gq[threadIdx.x + i * kThreads];
+#endif
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;   // (segment path: every lane is valid)
@@ -408,15 +423,32 @@ __global__ __launch_bounds__(kThreads) K1_ATTR void k_vit_approx(VitConsts vc, c
         int4 acc = make_int4(0, kNeg32, kNeg32, 0);
         const BlockWords bw = load_block(pk, k);
         const bool first = k == 0;
-        pipelined<4, 64>(
+#if VIT_K1_SLIM
+        // block 0's first window (3 steps: position 0 carries none) from the global table,
+        // multiplied in the same order as the other windows; its ring slot is skipped below
+        if (first) acc = i4_mul(acc, gq[1024u + (((bw.w[0] << 2) & 0x3FFu) >> 2)]);
+#endif
+#ifndef VIT_K1_LOOK
+#define VIT_K1_LOOK 4
+#endif
+        pipelined<VIT_K1_LOOK, 64>(
             [&](int j) {   // 5-base window of steps 4j .. 4j+3
                 const int r = j >> 2, s = j & 3;
                 const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
                 const uint32_t wi = s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 0x3FFu)
                                            : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
+#if VIT_K1_SLIM
+                return wi;
+#else
                 return (j == 0 && first) ? 1024u + (wi >> 2) : wi;
+#endif
             },
+#if VIT_K1_SLIM
+            [&](uint32_t wi) { return Q4[wi]; },
+            [&](const int4 q, int j) { if (j != 0 || !first) acc = i4_mul(acc, q); });
+#else
             [&](uint32_t wi) { return Q4[wi]; }, [&](const int4 q, int) { acc = i4_mul(acc, q); });
+#endif
         if (as.agg) {   // segment path (whole blocks only)
             approx_segment(vc, g, pk, c, k, CI{acc.x, acc.y, acc.z, acc.w}, as);
             return;
