@@ -205,6 +205,10 @@ def main():
                     help="pipeline lanes: step k runs on lane k %% lanes, each lane with its own "
                          "context (workspace), stream pair and outputs, so consecutive steps' "
                          "kernels of the same kind may run concurrently")
+    ap.add_argument("--train-lanes", type=int, default=1,
+                    help="training passes of consecutive steps alternate over this many "
+                         "contexts (workspaces) and CU-masked streams, so that step k+1's pass "
+                         "may start on the CUs step k's last round of workgroups leaves idle")
     ap.add_argument("--train-cus", type=int, default=-1,
                     help="run the training pass on this many compute units only (a CU-masked "
                          "stream, the first bits of the mask), leaving the rest to the decode; "
@@ -354,9 +358,18 @@ def main():
             ln["parts"].append({"ctx": cx2, "s": torch.cuda.Stream(priority=-1 if args.prio else 0),
                                 "iout": torch.empty((icap, 32), dtype=torch.uint8, device=dev),
                                 "icnt": torch.zeros(1, dtype=torch.int64, device=dev)})
+    ntl = 1 if (args.serial or args.no_overlap) else max(1, args.train_lanes)
+
+    def train_stream():
+        return (main_s if args.serial else
+                D.cu_stream(local, tr_cus) if tr_cus else torch.cuda.Stream())
     for ln in lanes:
-        ln["s_tr"] = (main_s if args.serial else
-                      D.cu_stream(local, tr_cus) if tr_cus else torch.cuda.Stream())
+        ln["s_tr"] = train_stream()
+        ln["tr"] = [(ln["ctx"], ln["s_tr"])]
+        for _ in range(1, ntl):
+            cx3 = Context(local)
+            cx3.reserve(N)
+            ln["tr"].append((cx3, train_stream()))
         # the decode stream at high priority: its latency-bound kernels get CUs first as the
         # E-step's workgroups retire, the E-step fills the rest
         ln["s_dec"] = main_s if args.serial else torch.cuda.Stream(priority=-1 if args.prio else 0)
@@ -422,6 +435,7 @@ def main():
                         torch.cuda._sleep(probe[1])
         par = k & 1
         rec, ecnt, lcnt = ln["recs"][par]
+        cx, s_tr = ln["tr"][k % ntl]   # (the decode above ran on the lane's own context)
         with torch.cuda.stream(s_tr):
             if dist and k >= 2:   # this record's previous all-gather has read it
                 s_tr.wait_event(ln["ev_red"][par])
@@ -470,7 +484,8 @@ def main():
         step(it, it)
     issue = time.perf_counter() - t0   # host time to enqueue every step (launch-bound check)
     for ln in lanes:
-        main_s.wait_stream(ln["s_tr"])
+        for _, st in ln["tr"]:
+            main_s.wait_stream(st)
         main_s.wait_stream(ln["s_dec"])
         main_s.wait_stream(ln["s_red"])
         for part in ln["parts"]:
@@ -488,6 +503,8 @@ def main():
     elapsed = time.perf_counter() - t0
     for ln in lanes:
         ln["ctx"].sync(None)     # raises if any kernel self-check (exactness) failed
+        for cx3, _ in ln["tr"][1:]:
+            cx3.sync(None)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -557,6 +574,7 @@ def main():
                           "decode_priority": "high" if (args.prio and not args.serial) else "normal",
                           "step_overlap": not (args.no_overlap or args.serial),
                           "pipeline_lanes": nlanes,
+                          "train_lanes": ntl,
                           "phase_events": ("all" if full_ev else
                                            f"estep every {args.estep_event_every}, decode every {args.decode_event_every}"),
                           "train_cus": len(tr_cus) if tr_cus else ncu,
@@ -584,8 +602,11 @@ def main():
             out["cpu_baseline"] = None
         print(json.dumps(out), flush=True)
     for ln in lanes:
-        if tr_cus:
-            D.cu_stream_destroy(ln["s_tr"])
+        for cx3, st in ln["tr"]:
+            if tr_cus:
+                D.cu_stream_destroy(st)
+            if cx3 is not ln["ctx"]:
+                cx3.close()
         for part in ln["parts"]:
             part["ctx"].close()
         ln["ctx"].close()
