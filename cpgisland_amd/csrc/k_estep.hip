@@ -58,7 +58,20 @@ constexpr int kAccRep = EST_ACC_REP;
 // (per-wave replicated sets, measured earlier, collide whenever two lanes of a pass share a
 // class).
 // LDS: TA/TB (512 B) | union { 4-step tables, scan buffer, bins } | per-wave partials
+#ifndef EST_STATIC_T
+#define EST_STATIC_T 0
+#endif
+#ifndef EST_INIT_AFTER
+#define EST_INIT_AFTER 0
+#endif
+#if EST_STATIC_T
+// TA/TB as a static LDS array: its offset is known when the kernel is compiled, so a table
+// row's address is the code times 16 with the base in the instruction's offset field (one
+// add fewer per forward position than with the dynamic array's base)
+constexpr size_t kUnionOff = 0;
+#else
 constexpr size_t kUnionOff = 32 * 16;
+#endif
 constexpr size_t kUnionBytes = 2048 * 16;
 __device__ __forceinline__ int bin_of(int d, int k) { return k * 16 + d; }
 
@@ -307,11 +320,18 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves
     // conflict-free constant tables: 16 x 16 B each = one 256-B bank row
+#if EST_STATIC_T
+    __shared__ __attribute__((aligned(256))) double2 sTAB[32];
+    double2* TA = sTAB;                                       // (M(+,+), M(+,-))
+    double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
+    double2* TA4 = reinterpret_cast<double2*>(smem);          // 4-step products, row 0
+#else
     double2* TA = reinterpret_cast<double2*>(smem);          // (M(+,+), M(+,-))
     double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
     // one union region after TA/TB, used in turn by: the 4-step tables (phase 1), the scan
     // buffer (phase 2), the xi bins (phase 3) — each phase ends with a barrier
     double2* TA4 = TB + 16;                                   // 4-step products, row 0
+#endif
     double2* TB4 = TA4 + 1024;                                //                  row 1
     auto* bins = reinterpret_cast<unsigned long long*>(TA4);  // [64 rows][16 columns]
     auto* part = reinterpret_cast<unsigned long long*>(
@@ -633,6 +653,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
                               mb = qb[(hi - 1 - i) % (EST_PFD + 1)];
                 if (t == 0 && m == 0 && i == 0) {   // gamma_0 = a_0 * y_0 / 2^47 -> init counts,
                     // added at once (nothing stays live across the main loop for it)
+#if EST_INIT_AFTER   // (after the loop: no global atomics in the loop body)
+                    continue;
+#endif
                     const uint32_t b0 = pk[0] & 3u;
                     unsigned long long* ra = acc + 2 * kSlab * (c % kAccRep);
                     acc128_add(ra + 2 * (64 + b0), to_fixed_scaled(alP[0] * yP), false);
@@ -686,6 +709,14 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         backward(0, kH);
 #endif
     }
+#if EST_INIT_AFTER
+    if (t == 0) {   // lane 0 ends at position 0: y = y_0 (its update was skipped), a_0 = fck[0]
+        const double2 a0 = fck[0];
+        const uint32_t b0 = pk[0] & 3u;
+        acc128_add(racc + 2 * (64 + b0), to_fixed_scaled(a0.x * yP), false);
+        acc128_add(racc + 2 * (64 + b0 + 4), to_fixed_scaled(a0.y * yM), false);
+    }
+#endif
 #ifdef CPG_STAMP_ESTEP
     if (lane == 0 && (c == 0 || c == 300 || c == 700) && (t >> 6) % 5 == 0)
         printf("stamp c%lld w%d: fwd16 %llu bwd8 %llu fwd8 %llu bwd8 %llu (cycles, 4 mini-blocks)\n",
