@@ -61,6 +61,9 @@ constexpr int kAccRep = EST_ACC_REP;
 #ifndef EST_STATIC_T
 #define EST_STATIC_T 0
 #endif
+#ifndef EST_PRIO
+#define EST_PRIO 0
+#endif
 #ifndef EST_INIT_AFTER
 #define EST_INIT_AFTER 0
 #endif
@@ -316,6 +319,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
                    unsigned int* done, double* __restrict__ out,
                    const uint32_t* __restrict__ sign, unsigned long long* __restrict__ cacc,
                    int64_t* __restrict__ cout) {
+#if EST_PRIO   // measurement knob: the E-step's waves raise their issue priority
+    __builtin_amdgcn_s_setprio(EST_PRIO);
+#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves

@@ -286,6 +286,16 @@ __device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
     return reinterpret_cast<const VitDerived*>(vt + 1);
 }
 
+// measurement knob: decode waves raise their issue priority (s_setprio) over the co-resident
+// E-step waves, which the SIMD's oldest-first arbitration otherwise favours
+#ifndef VIT_PRIO
+#define VIT_PRIO 0
+#endif
+#if VIT_PRIO
+#define VIT_PRIO_RAISE() __builtin_amdgcn_s_setprio(VIT_PRIO)
+#else
+#define VIT_PRIO_RAISE() ((void)0)
+#endif
 // Waves per SIMD a kernel is compiled for (VGPR budget 512 / n).  On a training CU the
 // E-step holds 4 waves x 96 VGPRs per SIMD, leaving 128: a decode kernel of <= 64 VGPRs gets
 // two wave slots there instead of one.  K5 (the longest decode kernel under overlap) is built
@@ -391,6 +401,7 @@ __device__ __forceinline__ VitPlan classify(const VitConsts& vc, const Geo& g, i
 __global__ __launch_bounds__(kThreads) K1_ATTR void k_vit_approx(VitConsts vc, const uint32_t* packed,
                                                          Geo g, const VitTables* vt,
                                                          int4* __restrict__ comp, ApproxSeg as) {
+    VIT_PRIO_RAISE();
     __shared__ int4 Q[16];
     // 4-step products over 5-base windows b0..b4 (exact: integers) [0, 1024), then the
     // 3-step products of steps 1..3 over b1..b4 [1024, 1280): block 0's first window (the
@@ -735,6 +746,7 @@ __global__ __launch_bounds__(kThreads) K3_ATTR void k_vit_exact(VitConsts vc, co
                                                         SegSum* __restrict__ seg,
                                                         const int32_t* __restrict__ irrseg,
                                                         double2* __restrict__ vhead) {
+    VIT_PRIO_RAISE();
     // per binade slot: single-step halves sA/sB [16] (one 256-B bank row each) and 2-step
     // composites over 3-base windows, halves P2A = (pp, pm), P2B = (mp, mm) [64].  Every
     // entry is a sum of binade-rounded constants: exact on the binade's grid.
@@ -1470,6 +1482,7 @@ __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
     const double4* __restrict__ rx, const SegSum* __restrict__ seg, double2* __restrict__ entry,
     double2* __restrict__ went, double4* __restrict__ gap, int32_t* __restrict__ barlist,
     double2* __restrict__ vout, const double2* __restrict__ vhead) {
+    VIT_PRIO_RAISE();
     const int64_t c = blockIdx.x;
     const int t = threadIdx.x;
     const int nseg = (int)(g.nsb / kThreads);
@@ -1979,6 +1992,7 @@ __global__ __launch_bounds__(kThreads) K5_ATTR void k_vit_forward(VitConsts vc, 
                                                           unsigned int* done,
                                                           uint8_t* __restrict__ endst,
                                                           double* __restrict__ score) {
+    VIT_PRIO_RAISE();
     // conflict-free halves (16 x 16 B each); entry 16 is the identity step (0, -inf, -inf,
     // 0) standing for block 0's position 0: P + 0.0 = P and M + -inf = -inf exactly, so the
     // values, the tie bits that matter and the origins are unchanged by it
@@ -2087,6 +2101,7 @@ __global__ __launch_bounds__(kThreads) K7_ATTR void k_vit_trace(Geo g, const uin
                                                         int64_t zero_n,
                                                         const uint32_t* __restrict__ packed,
                                                         IslFuse fz) {
+    VIT_PRIO_RAISE();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     // the undecoded tail's sign words ('-'), in this launch rather than a memset of its own
     for (int64_t i = gid; i < zero_n; i += (int64_t)gridDim.x * kThreads) zero_at[i] = 0u;
