@@ -205,6 +205,10 @@ def main():
                     help="pipeline lanes: step k runs on lane k %% lanes, each lane with its own "
                          "context (workspace), stream pair and outputs, so consecutive steps' "
                          "kernels of the same kind may run concurrently")
+    ap.add_argument("--decode-lanes", type=int, default=1,
+                    help="decodes of consecutive steps alternate over this many contexts, "
+                         "streams and output buffers, so that two steps' per-chunk kernels may "
+                         "run concurrently")
     ap.add_argument("--train-lanes", type=int, default=1,
                     help="training passes of consecutive steps alternate over this many "
                          "contexts (workspaces) and CU-masked streams, so that step k+1's pass "
@@ -359,6 +363,7 @@ def main():
                                 "iout": torch.empty((icap, 32), dtype=torch.uint8, device=dev),
                                 "icnt": torch.zeros(1, dtype=torch.int64, device=dev)})
     ntl = 1 if (args.serial or args.no_overlap) else max(1, args.train_lanes)
+    ndl = 1 if (args.serial or args.no_overlap) else max(1, args.decode_lanes)
 
     def train_stream():
         return (main_s if args.serial else
@@ -373,13 +378,21 @@ def main():
         # the decode stream at high priority: its latency-bound kernels get CUs first as the
         # E-step's workgroups retire, the E-step fills the rest
         ln["s_dec"] = main_s if args.serial else torch.cuda.Stream(priority=-1 if args.prio else 0)
+        ln["dec"] = [(ln["ctx"], ln["s_dec"], ln["so"], ln["score"], ln["iout"], ln["icnt"])]
+        for _ in range(1, ndl):
+            cx4 = Context(local)
+            cx4.reserve(N)
+            ln["dec"].append((cx4, torch.cuda.Stream(priority=-1 if args.prio else 0),
+                              torch.empty_like(ln["so"]), torch.empty_like(ln["score"]),
+                              torch.empty_like(ln["iout"]), torch.zeros_like(ln["icnt"])))
         # the reducer's collective on a stream of its own: the next step's training pass does
         # not wait for it
         ln["s_red"] = main_s if args.serial else torch.cuda.Stream()
 
     def step(it, k):
         ln = lanes[k % nlanes]
-        cx, s_tr, s_dec = ln["ctx"], ln["s_tr"], ln["s_dec"]
+        cx, s_tr = ln["ctx"], ln["s_tr"]
+        dcx, s_dec, d_so, d_score, d_iout, d_icnt = ln["dec"][k % ndl]
 
         def mark(name, i):
             if it is None or args.no_phase_events:
@@ -409,21 +422,21 @@ def main():
             nb = (c1 - c0) * DECODE if pi < nsplit - 1 else N - c0 * DECODE
             part = ln["parts"][pi - 1] if pi > 0 else None
             with torch.cuda.stream(part["s"] if part else s_dec):
-                px = part["ctx"] if part else cx
-                pp, sg = dp[c0 * DECODE // 16:], ln["so"][c0 * DECODE // 32:]
-                io = part["iout"] if part else ln["iout"]
-                ic = part["icnt"] if part else ln["icnt"]
+                px = part["ctx"] if part else dcx
+                pp, sg = dp[c0 * DECODE // 16:], d_so[c0 * DECODE // 32:]
+                io = part["iout"] if part else d_iout
+                ic = part["icnt"] if part else d_icnt
                 if fused_decode:
                     if pi == 0:
                         mark("decode", 0)
                     D.decode(px, model1, pp, nb, DECODE, cap=icap, first_chunk=first_chunk + c0,
-                             sign_out=sg, score=ln["score"][c0:], out=io, count=ic)
+                             sign_out=sg, score=d_score[c0:], out=io, count=ic)
                     if pi == 0:
                         mark("decode", 1)
                 else:
                     if pi == 0:
                         mark("viterbi", 0)
-                    D.viterbi(px, model1, pp, nb, DECODE, sign_out=sg, score=ln["score"][c0:])
+                    D.viterbi(px, model1, pp, nb, DECODE, sign_out=sg, score=d_score[c0:])
                     if pi == 0:
                         mark("viterbi", 1)
                         mark("islands", 0)
@@ -486,7 +499,8 @@ def main():
     for ln in lanes:
         for _, st in ln["tr"]:
             main_s.wait_stream(st)
-        main_s.wait_stream(ln["s_dec"])
+        for dl in ln["dec"]:
+            main_s.wait_stream(dl[1])
         main_s.wait_stream(ln["s_red"])
         for part in ln["parts"]:
             main_s.wait_stream(part["s"])
@@ -505,6 +519,8 @@ def main():
         ln["ctx"].sync(None)     # raises if any kernel self-check (exactness) failed
         for cx3, _ in ln["tr"][1:]:
             cx3.sync(None)
+        for dl in ln["dec"][1:]:
+            dl[0].sync(None)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -575,6 +591,7 @@ def main():
                           "step_overlap": not (args.no_overlap or args.serial),
                           "pipeline_lanes": nlanes,
                           "train_lanes": ntl,
+                          "decode_lanes": ndl,
                           "phase_events": ("all" if full_ev else
                                            f"estep every {args.estep_event_every}, decode every {args.decode_event_every}"),
                           "train_cus": len(tr_cus) if tr_cus else ncu,
@@ -607,6 +624,8 @@ def main():
                 D.cu_stream_destroy(st)
             if cx3 is not ln["ctx"]:
                 cx3.close()
+        for dl in ln["dec"][1:]:
+            dl[0].close()
         for part in ln["parts"]:
             part["ctx"].close()
         ln["ctx"].close()
