@@ -75,7 +75,17 @@ constexpr size_t kUnionOff = 0;
 #else
 constexpr size_t kUnionOff = 32 * 16;
 #endif
+#ifndef EST_TAB_IN_CKPT
+#define EST_TAB_IN_CKPT 0
+#endif
+#if EST_TAB_IN_CKPT
+// the 4-step tables (phase 1) live in the alpha-checkpoint region, which is written only
+// after the scans: the union holds just the scan buffer and the xi bins (8 KB), 24 KB less LDS
+// per workgroup for decode workgroups on the same CU
+constexpr size_t kUnionBytes = 64 * 16 * 8;
+#else
 constexpr size_t kUnionBytes = 2048 * 16;
+#endif
 __device__ __forceinline__ int bin_of(int d, int k) { return k * 16 + d; }
 
 struct Mat {
@@ -338,11 +348,15 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     // buffer (phase 2), the xi bins (phase 3) — each phase ends with a barrier
     double2* TA4 = TB + 16;                                   // 4-step products, row 0
 #endif
-    double2* TB4 = TA4 + 1024;                                //                  row 1
-    auto* bins = reinterpret_cast<unsigned long long*>(TA4);  // [64 rows][16 columns]
     auto* part = reinterpret_cast<unsigned long long*>(
         smem + kUnionOff + kUnionBytes);
     double2* fck = reinterpret_cast<double2*>(part + 16 * 64);   // [NMB][nl] alpha checkpoints
+    unsigned char* uni = smem + kUnionOff;   // scan buffer (phase 2), xi bins (phase 3)
+#if EST_TAB_IN_CKPT
+    TA4 = fck;
+#endif
+    double2* TB4 = TA4 + 1024;                                //                  row 1
+    auto* bins = reinterpret_cast<unsigned long long*>(uni);  // [64 rows][16 columns]
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int64_t c = blockIdx.x;
@@ -468,7 +482,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     const Mat I1 = mid();
     const Mat up1 = dpp_mat<0x138>(xp, I1), dn1 = dpp_mat<0x130>(xs, I1);   // wave_shr/shl:1
     __syncthreads();   // every lane is past its 4-step table reads: the union is free
-    Mat* sWP = reinterpret_cast<Mat*>(TA4);   // [16] wave products (prefix order)
+    Mat* sWP = reinterpret_cast<Mat*>(uni);   // [16] wave products (prefix order)
     Mat* sWS = sWP + 16;                      // [16] wave products (suffix order)
     Mat* sXP = sWS + 16;                      // [17] products of the waves before; [16] all
     Mat* sXS = sXP + 17;                      // [16] products of the waves after
@@ -848,8 +862,10 @@ namespace {
 #define CPG_EST_LDS_PAD 0   // measurement only: extra LDS per workgroup (co-residency probe)
 #endif
 size_t estep_lds(int lanes) {   // the union is sized for 16 waves; fewer lanes use a prefix
+    const size_t ck = (size_t)(kLanePos / 16) * lanes * sizeof(double2);
     return kUnionOff + kUnionBytes + 16 * 64 * sizeof(unsigned long long) +
-           (size_t)(kLanePos / 16) * lanes * sizeof(double2) + CPG_EST_LDS_PAD;
+           (EST_TAB_IN_CKPT ? std::max(ck, (size_t)2048 * sizeof(double2)) : ck) +
+           CPG_EST_LDS_PAD;
 }
 }  // namespace
 

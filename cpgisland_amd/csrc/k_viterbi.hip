@@ -286,6 +286,24 @@ __device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
     return reinterpret_cast<const VitDerived*>(vt + 1);
 }
 
+// measurement knob: extra static LDS per workgroup of K1 / K3 / K7 (bytes), so that those
+// kernels cannot share a CU with the E-step (co-residency probe)
+#define VIT_LDS_PAD(n)                                                                     \
+    __shared__ volatile unsigned char vit_pad_[(n) > 0 ? (n) : 1];                          \
+    {                                                                                      \
+        int z_ = threadIdx.x;                                                              \
+        asm volatile("" : "+v"(z_));                                                       \
+        if (z_ == 0x7fffffff) vit_pad_[z_ & 1] = 0;                                        \
+    }
+#ifndef VIT_PAD_K1
+#define VIT_PAD_K1 0
+#endif
+#ifndef VIT_PAD_K3
+#define VIT_PAD_K3 0
+#endif
+#ifndef VIT_PAD_K7
+#define VIT_PAD_K7 0
+#endif
 // measurement knob: decode waves raise their issue priority (s_setprio) over the co-resident
 // E-step waves, which the SIMD's oldest-first arbitration otherwise favours
 #ifndef VIT_PRIO
@@ -402,6 +420,9 @@ __global__ __launch_bounds__(kThreads) K1_ATTR void k_vit_approx(VitConsts vc, c
                                                          Geo g, const VitTables* vt,
                                                          int4* __restrict__ comp, ApproxSeg as) {
     VIT_PRIO_RAISE();
+#if VIT_PAD_K1
+    VIT_LDS_PAD(VIT_PAD_K1)
+#endif
     __shared__ int4 Q[16];
     // 4-step products over 5-base windows b0..b4 (exact: integers) [0, 1024), then the
     // 3-step products of steps 1..3 over b1..b4 [1024, 1280): block 0's first window (the
@@ -747,6 +768,9 @@ __global__ __launch_bounds__(kThreads) K3_ATTR void k_vit_exact(VitConsts vc, co
                                                         const int32_t* __restrict__ irrseg,
                                                         double2* __restrict__ vhead) {
     VIT_PRIO_RAISE();
+#if VIT_PAD_K3
+    VIT_LDS_PAD(VIT_PAD_K3)
+#endif
     // per binade slot: single-step halves sA/sB [16] (one 256-B bank row each) and 2-step
     // composites over 3-base windows, halves P2A = (pp, pm), P2B = (mp, mm) [64].  Every
     // entry is a sum of binade-rounded constants: exact on the binade's grid.
@@ -2102,6 +2126,9 @@ __global__ __launch_bounds__(kThreads) K7_ATTR void k_vit_trace(Geo g, const uin
                                                         const uint32_t* __restrict__ packed,
                                                         IslFuse fz) {
     VIT_PRIO_RAISE();
+#if VIT_PAD_K7
+    VIT_LDS_PAD(VIT_PAD_K7)
+#endif
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     // the undecoded tail's sign words ('-'), in this launch rather than a memset of its own
     for (int64_t i = gid; i < zero_n; i += (int64_t)gridDim.x * kThreads) zero_at[i] = 0u;
