@@ -222,12 +222,13 @@ def main():
                     help="with --train-cus: leave out every k-th CU instead of the last ones")
     ap.add_argument("--phase-events", action="store_true",
                     help="record HIP events around every phase (default: E-step and decode)")
-    ap.add_argument("--decode-event-every", type=int, default=4,
+    ap.add_argument("--decode-event-every", type=int, default=16,
                     help="record the decode phase's events on every k-th timed step")
-    ap.add_argument("--estep-event-every", type=int, default=4,
+    ap.add_argument("--estep-event-every", type=int, default=16,
                     help="record the E-step phase's events on every k-th timed step (an event "
-                         "record is a release at its point in the stream: ~6 us of train-stream "
-                         "gap each)")
+                         "record is a release at its point in the stream: every 4th step cost "
+                         "1.5 %% of the rate against none, every 16th 0.9 %%; 25 samples per "
+                         "400 steps)")
     ap.add_argument("--no-phase-events", action="store_true",
                     help="(diagnostic) record no per-phase HIP events inside the timed steps")
     ap.add_argument("--decode-split", type=int, default=1,
@@ -318,7 +319,8 @@ def main():
     # the decode phase (on every --decode-event-every-th step) by default; every phase with
     # --phase-events or --serial.  An event record is not free (a release at the stream's
     # point of record): 10 per step cost ~9 % of the overlapped throughput, 4 per step ~3 %,
-    # the E-step's 2 per step plus the decode's on every 4th step ~1 %.
+    # both phases' on every 4th step 1.5 %, on every 16th 0.9 % (the default: 25 samples of
+    # each phase per 400 steps; profiles/r02_v10/ab_phase_events.log).
     full_ev = args.phase_events or args.serial
     probe = None
     if args.probe_sleep:
