@@ -218,6 +218,9 @@ def main():
                          "stream, the first bits of the mask), leaving the rest to the decode; "
                          "0 = all, -1 = 14/16 of them (default; with the fused decode a 400-step "
                          "sweep read 192: 274, 208: 276, 216: 277, 224: 280, 232: 270, 240: 262)")
+    ap.add_argument("--decode-cus-from", type=int, default=0,
+                    help="> 0: the decode stream CU-masked to compute units [this, all) (a masked "
+                         "stream has no priority: the decode then runs at normal priority)")
     ap.add_argument("--train-cu-stride", type=int, default=0,
                     help="with --train-cus: leave out every k-th CU instead of the last ones")
     ap.add_argument("--phase-events", action="store_true",
@@ -379,7 +382,10 @@ def main():
             ln["tr"].append((cx3, train_stream()))
         # the decode stream at high priority: its latency-bound kernels get CUs first as the
         # E-step's workgroups retire, the E-step fills the rest
-        ln["s_dec"] = main_s if args.serial else torch.cuda.Stream(priority=-1 if args.prio else 0)
+        ln["s_dec"] = (main_s if args.serial else
+                       D.cu_stream(local, list(range(args.decode_cus_from, ncu)))
+                       if args.decode_cus_from > 0 else
+                       torch.cuda.Stream(priority=-1 if args.prio else 0))
         ln["dec"] = [(ln["ctx"], ln["s_dec"], ln["so"], ln["score"], ln["iout"], ln["icnt"])]
         for _ in range(1, ndl):
             cx4 = Context(local)
@@ -594,6 +600,7 @@ def main():
                           "pipeline_lanes": nlanes,
                           "train_lanes": ntl,
                           "decode_lanes": ndl,
+                          "decode_cus_from": args.decode_cus_from,
                           "phase_events": ("all" if full_ev else
                                            f"estep every {args.estep_event_every}, decode every {args.decode_event_every}"),
                           "train_cus": len(tr_cus) if tr_cus else ncu,
@@ -628,6 +635,8 @@ def main():
                 cx3.close()
         for dl in ln["dec"][1:]:
             dl[0].close()
+        if args.decode_cus_from > 0 and not args.serial:
+            D.cu_stream_destroy(ln["s_dec"])
         for part in ln["parts"]:
             part["ctx"].close()
         ln["ctx"].close()
