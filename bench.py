@@ -395,7 +395,10 @@ def main():
                               torch.empty_like(ln["iout"]), torch.zeros_like(ln["icnt"])))
         # the reducer's collective on a stream of its own: the next step's training pass does
         # not wait for it
-        ln["s_red"] = main_s if args.serial else torch.cuda.Stream()
+        # (N = 1: no reducer, no stream: a HIP stream's hardware queue is created on its first
+        # use, and that took ~5 ms of host time plus a disturbance of the running queues when
+        # the first use was the final join of the timed region — profiles/r03_v1)
+        ln["s_red"] = main_s if (args.serial or not dist) else torch.cuda.Stream()
 
     def step(it, k):
         ln = lanes[k % nlanes]
@@ -498,31 +501,56 @@ def main():
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
+    # CPG_BENCH_TIMELINE=1: host timeline of the timed region's end and the GPU span of the
+    # timed steps (events on the training and decode streams before step 0 / after the last)
+    gpu_span = ([], []) if os.environ.get("CPG_BENCH_TIMELINE") else None
     t0 = time.perf_counter()
+    if gpu_span is not None:
+        for ln in lanes:
+            for _, st in ln["tr"] + [(None, ln["s_dec"])]:
+                gpu_span[0].append(torch.cuda.Event(enable_timing=True))
+                gpu_span[0][-1].record(st)
     for it in range(args.steps):
         if flush is not None:
             flush.fill_(1.0)
         step(it, it)
     issue = time.perf_counter() - t0   # host time to enqueue every step (launch-bound check)
-    for ln in lanes:
-        for _, st in ln["tr"]:
-            main_s.wait_stream(st)
-        for dl in ln["dec"]:
-            main_s.wait_stream(dl[1])
-        main_s.wait_stream(ln["s_red"])
-        for part in ln["parts"]:
-            main_s.wait_stream(part["s"])
+    tl = [("issued", issue)]
+    # the end of the timed region: one device-wide synchronize waits for every stream of
+    # every lane (no per-stream joins: a join records an event on each stream, and a stream
+    # never used before — the N = 1 reducer stream — created its hardware queue right there)
+    if gpu_span is not None:
+        for ln in lanes:
+            for _, st in ln["tr"]:
+                gpu_span[1].append(torch.cuda.Event(enable_timing=True))
+                gpu_span[1][-1].record(st)
+            gpu_span[1].append(torch.cuda.Event(enable_timing=True))
+            gpu_span[1][-1].record(ln["s_dec"])
+    tl.append(("joined", time.perf_counter() - t0))
     torch.cuda.synchronize()
+    tl.append(("sync1", time.perf_counter() - t0))
     nrec = {k: 0 for k in names}
     for it, ev in enumerate(evs):
         for k, (a, b) in ev.items():
             if (it, k) in recorded:
                 acc[k] += a.elapsed_time(b)
                 nrec[k] += 1
+    tl.append(("events", time.perf_counter() - t0))
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    tl.append(("sync2", elapsed))
+    if gpu_span is not None:
+        a0 = gpu_span[0][0]
+        span = max(a0.elapsed_time(e) for e in gpu_span[1]) - \
+            min(a0.elapsed_time(e) for e in gpu_span[0])
+        log("timeline ms: " + " ".join(f"{k}={v * 1e3:.3f}" for k, v in tl) +
+            f" gpu_span={span:.3f}")
+        for k in names:   # per-step phase durations in order (the warm-up of the clocks)
+            ser = [round(ev[k][0].elapsed_time(ev[k][1]), 4) for it, ev in enumerate(evs)
+                   if (it, k) in recorded]
+            log(f"phase {k}: {ser}")
     for ln in lanes:
         ln["ctx"].sync(None)     # raises if any kernel self-check (exactness) failed
         for cx3, _ in ln["tr"][1:]:

@@ -586,14 +586,13 @@ int cpg_decode_states(cpg_ctx* ctx, const cpg_model* model, const int32_t* obs, 
     std::vector<uint32_t> sign((size_t)(n + 31) / 32 + 4, 0u);
     double score = 0.0;
     CPG_TRY(cpg_viterbi(ctx, model, packed.data(), n, n, sign.data(), &score));
-    // pi = 0 for both live states at t=0: Mahout's maxState stays 0 (state A+) at every
-    // step (all candidates are -Double.MAX_VALUE); the '+' sign path is right, the indices
-    // are not the base's: patch them (the final argmax still picks o_{T-1}+ when T > 1).
+    // pi = 0 for both live states at t=0: every candidate is -inf, Mahout's maxState stays 0
+    // (state A+) at every step and the final argmax (strict '>' from -inf) leaves state 0
+    // (SURVEY.md A.2); the '+' sign path is right, the indices are not the base's: patch them
     const bool degen = model->pi[obs[0]] == 0.0 && model->pi[obs[0] + 4] == 0.0;
     for (int64_t i = 0; i < n; ++i) {
         const bool plus = (sign[i >> 5] >> (i & 31)) & 1u;
-        states_out[i] = obs[i] + (plus ? 0 : 4);
-        if (degen && (i < n - 1 || n == 1)) states_out[i] = 0;
+        states_out[i] = degen ? 0 : obs[i] + (plus ? 0 : 4);
     }
     return CPG_OK;
 }

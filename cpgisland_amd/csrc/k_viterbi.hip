@@ -1175,8 +1175,8 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     __shared__ double4 stageL[kStageSteps];
     if (t < 16) sL[t] = make_double4(vc.L[t][0], vc.L[t][1], vc.L[t][2], vc.L[t][3]);
     if (degen[c]) {
-        for (int64_t k = b0; k < b1; ++k) ent[k] = make_double2(-DBL_MAX, -DBL_MAX);
-        if (t == kChainT - 1) ent[g.nsb] = make_double2(-DBL_MAX, -DBL_MAX);
+        for (int64_t k = b0; k < b1; ++k) ent[k] = make_double2(-INFINITY, -INFINITY);
+        if (t == kChainT - 1) ent[g.nsb] = make_double2(-INFINITY, -INFINITY);
         return;
     }
     const uint32_t* pk = chunk_ptr(packed, g, c);
@@ -1513,8 +1513,8 @@ __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
     const int64_t s0 = c * nseg;
     double2* ent = entry + c * (g.nsb + 1);
     if (degen[c]) {
-        for (int w = t; w < nseg; w += kSegT) went[s0 + w] = make_double2(-DBL_MAX, -DBL_MAX);
-        if (t == 0) ent[g.nsb] = make_double2(-DBL_MAX, -DBL_MAX);
+        for (int w = t; w < nseg; w += kSegT) went[s0 + w] = make_double2(-INFINITY, -INFINITY);
+        if (t == 0) ent[g.nsb] = make_double2(-INFINITY, -INFINITY);
         return;
     }
     const uint32_t* pk = chunk_ptr(packed, g, c);

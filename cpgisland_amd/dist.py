@@ -223,11 +223,13 @@ def shard_plan(start: int, n: int, nbases: int, train: int = _lib.TRAIN_CHUNK,
 
 def halo_exchange(packed: torch.Tensor, sign: torch.Tensor, n: int, group=None,
                   width: int = _lib.DECODE_CHUNK):
-    """All-gather of every rank's first `width` bases (packed and sign words, zero-padded);
-    returns the next rank's (packed head, sign head), or (None, None) on the last rank."""
+    """All-gather of every rank's first `width` bases (packed and sign words, zero-padded)
+    and of every rank's shard length; returns the next rank's (packed head, sign head, shard
+    length), or (None, None, 0) on the last rank.  The length lets local_buffers refuse a
+    halo that would run past the next rank's shard into its zero padding."""
     ws = _group_size(group)
     if ws == 1:
-        return None, None
+        return None, None, 0
     rank = dist.get_rank(group)
     w16, w32 = width // 16, width // 32
     hp = torch.zeros(w16, dtype=packed.dtype, device=packed.device)
@@ -237,21 +239,30 @@ def halo_exchange(packed: torch.Tensor, sign: torch.Tensor, n: int, group=None,
     hs[:k32] = sign[:k32]
     gp = [torch.empty_like(hp) for _ in range(ws)]
     gs = [torch.empty_like(hs) for _ in range(ws)]
+    nt = torch.tensor([n], dtype=torch.int64, device=packed.device)
+    gn = [torch.empty_like(nt) for _ in range(ws)]
     dist.all_gather(gp, hp, group=group)
     dist.all_gather(gs, hs, group=group)
+    dist.all_gather(gn, nt, group=group)
     if rank == ws - 1:
-        return None, None
-    return gp[rank + 1], gs[rank + 1]
+        return None, None, 0
+    return gp[rank + 1], gs[rank + 1], int(gn[rank + 1].item())
 
 
 def local_buffers(packed: torch.Tensor, sign: torch.Tensor, plan: ShardPlan,
-                  head_p: torch.Tensor | None, head_s: torch.Tensor | None):
+                  head_p: torch.Tensor | None, head_s: torch.Tensor | None,
+                  head_n: int | None = None):
     """The rank's packed / sign words of bases [plan.base, plan.end): its own words from
     plan.base, then the halo from the next rank's head (padded by 4 words, as the kernels'
-    buffers are)."""
+    buffers are).  head_n: the next rank's shard length (halo_exchange returns it); a halo
+    longer than it would take zero padding for bases, so it is refused."""
     if plan.halo and (head_p is None or plan.halo > head_p.numel() * 16):
         raise ValueError("the halo reaches past the next rank's head: shards must hold at "
                          "least one decode chunk")
+    if plan.halo and head_n is not None and plan.halo > head_n:
+        raise ValueError(f"the halo ({plan.halo} bases) runs past the next rank's shard "
+                         f"({head_n} bases): every shard but the last must hold at least "
+                         f"one decode chunk")
     off = plan.base - plan.start
     own = min(plan.start + plan.n, plan.end) - plan.base
     if own < 0 or off < 0:
@@ -272,10 +283,14 @@ class HaloShardRunner:
 
     def __init__(self, ctx, packed: torch.Tensor, sign: torch.Tensor, start: int, n: int,
                  nbases: int, group=None, heads=None):
+        """heads: (packed head, sign head, next shard length) as halo_exchange returns them
+        (None: run the exchange here)."""
         self.ctx, self.group = ctx, group
         self.plan = shard_plan(start, n, nbases)
-        hp, hs = heads if heads is not None else halo_exchange(packed, sign, n, group)
-        self.packed, self.sign = local_buffers(packed, sign, self.plan, hp, hs)
+        hd = heads if heads is not None else halo_exchange(packed, sign, n, group)
+        hp, hs = hd[0], hd[1]
+        hn = hd[2] if len(hd) > 2 else None
+        self.packed, self.sign = local_buffers(packed, sign, self.plan, hp, hs, hn)
 
     def _train_view(self):
         pl = self.plan

@@ -107,9 +107,12 @@ double orc_viterbi8(const cpg_model* m, const uint8_t* obs, int64_t T, int32_t* 
     for (int i = 0; i < 8; ++i) dprev[i] = log(m->pi[i] * m->b[i][obs[0]]);
     for (int64_t t = 1; t < T; ++t) {
         for (int i = 0; i < 8; ++i) {
+            /* Mahout's induction starts from candidate j = 0, not from a
+             * sentinel: when every candidate is -inf (pi = 0 for both live states at t = 0)
+             * delta stays -inf, maxState stays 0 and the final argmax leaves state 0 */
             int maxState = 0;
-            double maxProb = -DBL_MAX;
-            for (int j = 0; j < 8; ++j) {
+            double maxProb = dprev[0] + log(m->a[0][i]);
+            for (int j = 1; j < 8; ++j) {
                 double prob = dprev[j] + log(m->a[j][i]);
                 if (prob > maxProb) { maxProb = prob; maxState = j; }
             }

@@ -70,8 +70,8 @@ def viterbi8(pi, a, b, obs):
     for t in range(1, T):
         nd, row = [0.0] * 8, [0] * 8
         for i in range(8):
-            ms, mp = 0, -DBL_MAX
-            for j in range(8):
+            ms, mp = 0, delta[0] + _log(a[0][i])     # Mahout: candidate 0 first (A.2)
+            for j in range(1, 8):
                 p = delta[j] + _log(a[j][i])
                 if p > mp:
                     mp, ms = p, j

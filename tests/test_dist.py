@@ -147,8 +147,8 @@ def _halo_worker(rank, world, port, q):
         pk = torch.from_numpy(pr.pack(obs[start:start + n]).view(np.int32).copy())
         sg = torch.from_numpy(pr.pack_bits(truth[start:start + n]).view(np.int32).copy())
         plan = cd.shard_plan(start, n, N, train=TRAIN, decode=DECODE)
-        hp, hs = cd.halo_exchange(pk, sg, n, width=DECODE)
-        lp, ls = cd.local_buffers(pk, sg, plan, hp, hs)
+        hp, hs, hn = cd.halo_exchange(pk, sg, n, width=DECODE)
+        lp, ls = cd.local_buffers(pk, sg, plan, hp, hs, hn)
         span = plan.end - plan.base
         lo = pr.unpack(lp.numpy().view(np.uint32), span)
         lt = pr.unpack_bits(ls.numpy().view(np.uint32), span)
@@ -194,6 +194,23 @@ def test_unaligned_shards_with_halo_equal_unsharded(world):
         assert np.array_equal(r[5], res[0][5])
         assert np.max(np.abs(r[5][nz] - full_e[nz]) / np.abs(full_e[nz])) < 1e-12
         assert np.array_equal(r[6].view(co.ISLAND_DTYPE), isl)
+
+
+def test_halo_longer_than_next_shard_is_refused():
+    """a short middle shard cannot supply the previous rank's halo; the halo would
+    be read from the zero padding of its head (as base 'A'), so local_buffers raises."""
+    n_genome = 4 * DECODE
+    # rank 0: [0, DECODE + 64) owns decode chunk 0 and chunk 1 (first base DECODE) -> halo
+    plan = cd.shard_plan(0, DECODE + 64, n_genome, train=TRAIN, decode=DECODE)
+    assert plan.halo == DECODE - 64
+    pk = torch.zeros((DECODE + 64) // 16, dtype=torch.int32)
+    sg = torch.zeros((DECODE + 64) // 32, dtype=torch.int32)
+    hp = torch.zeros(DECODE // 16, dtype=torch.int32)
+    hs = torch.zeros(DECODE // 32, dtype=torch.int32)
+    with pytest.raises(ValueError, match="next rank's shard"):
+        cd.local_buffers(pk, sg, plan, hp, hs, 4096)          # next shard: 4096 bases only
+    lp, ls = cd.local_buffers(pk, sg, plan, hp, hs, DECODE)   # long enough: accepted
+    assert lp.numel() == (plan.end - plan.base) // 16 + 4
 
 
 @pytest.mark.parametrize("n,world", [(5 * DECODE + 1234, 2), (5 * DECODE + 1234, 4),

@@ -35,13 +35,13 @@ def test_halo_shards_equal_unsharded(gpu_ctx):
     isl, halos = [], []
     for r, (start, n) in enumerate(spans):
         p, s = D.synth_host(seed, start, n)          # the rank's own words
-        heads = (None, None)
+        heads = (None, None, 0)
         if r + 1 < world:                             # the next rank's first 2^20 bases
             s1, n1 = spans[r + 1]
             hp, hs = D.synth_host(seed, s1, min(n1, DECODE))
             hp = np.concatenate([hp, np.zeros(DECODE // 16, np.uint32)])[:DECODE // 16]
             hs = np.concatenate([hs, np.zeros(DECODE // 32, np.uint32)])[:DECODE // 32]
-            heads = (D.to_device(hp, dev), D.to_device(hs, dev))
+            heads = (D.to_device(hp, dev), D.to_device(hs, dev), n1)
         run = cd.HaloShardRunner(gpu_ctx, D.to_device(p, dev), D.to_device(s, dev), start, n,
                                  N, heads=heads)
         halos.append(run.plan.halo)

@@ -130,14 +130,18 @@ def test_kat_cg_repeat_decodes_plus_and_at_repeat_minus():
 
 
 def test_degenerate_pi_zero_path_is_state_zero():
-    """pi = 0 for both live states: Mahout keeps maxState = 0 at every step."""
+    """pi = 0 for both live states: every candidate is -inf, Mahout's maxProb starts at
+    candidate 0, so delta stays -inf, maxState stays 0 at every step and the
+    final argmax (strict '>' from -inf) leaves state 0: the path is all state 0 (A+)."""
     m = m0().copy()
     m[3] = 0.0
     m[7] = 0.0        # pi[T+] = pi[T-] = 0
     obs = np.array([3, 1, 2, 0, 3], np.uint8)
     st, best = co.viterbi8(m, obs)
-    assert list(st[:-1]) == [0, 0, 0, 0] and st[-1] == obs[-1]
-    assert best == -1.7976931348623157e308
+    assert list(st) == [0, 0, 0, 0, 0]
+    assert best == -np.inf
+    sg, b2 = co.viterbi2(m, obs)          # the 2-state form: all '+', score -inf
+    assert sg.all() and b2 == -np.inf
     seq, mp = pr.viterbi8(m[:8].tolist(), m[8:72].reshape(8, 8).tolist(),
                           m[72:].reshape(8, 4).tolist(), obs.tolist())
     assert seq == list(st)
