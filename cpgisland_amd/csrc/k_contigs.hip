@@ -295,10 +295,8 @@ __device__ __forceinline__ void acc128_add2(unsigned long long* lohi, unsigned l
     if (hi) atomicAdd(lohi + 1, hi);
 }
 
-#ifndef CTG_EST_WAVES
-#define CTG_EST_WAVES 3   // min waves per SIMD (VGPR budget 512 / this; 2..4 measured)
-#endif
-__global__ __launch_bounds__(kCT, CTG_EST_WAVES) void k_ctg_estep(Ctg a, cpg_model model,
+constexpr int kCtgEstWaves = 3;   // min waves per SIMD (VGPR budget 512 / this; 2..4 measured)
+__global__ __launch_bounds__(kCT, kCtgEstWaves) void k_ctg_estep(Ctg a, cpg_model model,
                                                    double2* __restrict__ ck,
                                                    unsigned long long* __restrict__ acc) {
     __shared__ double2 TA[16], TB[16];   // rows of M_d: (M(+,+), M(+,-)), (M(-,+), M(-,-))

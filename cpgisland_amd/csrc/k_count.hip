@@ -22,13 +22,8 @@ namespace {
 using cnt::kRaw;
 constexpr int kCountThreads = 256;
 constexpr int kCntRep = cnt::kRep;
-#ifndef CNT_GRID
-#define CNT_GRID 512   // measured: 2048 / 1024 / 512 workgroups 19.0 / 14.6 / 12.9 us at 46 Mbp
-#endif
-#ifndef CNT_BATCH
-#define CNT_BATCH 6    // blocks per lane in flight (46 Mbp: 5.5 blocks per lane at 512 x 256)
-#endif
-constexpr int kBatch = CNT_BATCH;
+constexpr int kCntGrid = 512;   // measured: 2048 / 1024 / 512 workgroups 19.0 / 14.6 / 12.9 us at 46 Mbp
+constexpr int kBatch = 6;       // blocks per lane in flight (46 Mbp: 5.5 blocks per lane at 512 x 256)
 static_assert(kBatch <= cnt::Lane::kMaxBlocks, "16-bit wave sums");
 
 // done != nullptr: the last workgroup to finish also finalizes (one launch per call)
@@ -42,10 +37,6 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
     __shared__ int s_last;
     const int t = threadIdx.x;
     const bool pow2 = (blk_per_chunk & (blk_per_chunk - 1)) == 0;
-#ifdef CNT_STAMP
-    const unsigned long long T0 = wall_clock64();
-    unsigned long long T1 = 0, T2 = 0;
-#endif
     if (t < kRaw) scnt[t] = 0u;
     __syncthreads();
     cnt::Lane lc;
@@ -71,15 +62,6 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
             wp[r] = packed[4 * ip + 3];
             sp[r] = sign[2 * ip + 1];
         }
-#ifdef CNT_STAMP
-        {
-            uint32_t x = 0;
-#pragma unroll
-            for (int r = 0; r < kBatch; ++r) x += w[r].x + s[r].y + wp[r] + sp[r];
-            if (x == 0x9999999u) scnt[0] = x;
-            T1 = wall_clock64();
-        }
-#endif
 #pragma unroll
         for (int r = 0; r < kBatch; ++r) {
             const int64_t i = i0 + r * stride;
@@ -90,37 +72,15 @@ __global__ __launch_bounds__(kCountThreads) void k_count_main(
                 lc.block(w[r], s[r], wp[r], sp[r] >> 31, cstart, scnt);
             }
         }
-#ifdef CNT_STAMP
-        T2 = wall_clock64();
-#endif
         lc.flush(scnt);   // per batch: kBatch <= Lane::kMaxBlocks
     }
     __syncthreads();
-#ifdef CNT_STAMP
-    const unsigned long long T3 = wall_clock64();
-#endif
     if (t < kRaw) {
         const uint32_t v = cnt::raw_of(scnt, t);
-#ifdef CNT_NOATOM   // measurement only: wrong counts
-        if (v == 0x12345678u)
-#else
         if (v)
-#endif
             atomicAdd(gacc + (blockIdx.x % kCntRep) * kRaw + t, (unsigned long long)v);
     }
-#ifdef CNT_STAMP
-    __builtin_amdgcn_s_waitcnt(0);
-    __syncthreads();
-    const unsigned long long T4 = wall_clock64();
-    if (t == 0 && (blockIdx.x % 64 == 0 || blockIdx.x == gridDim.x - 1))
-        printf("cnt wg %d: start %llu loads %llu count %llu flush+bar %llu atomics %llu\n",
-               blockIdx.x, T0 % 1000000, T1 - T0, T2 - T1, T3 - T2, T4 - T3);
-#endif
-#ifdef CNT_NOFIN   // measurement only: no finalize
-    if (done && blockIdx.x == 0x7fffffff) {
-#else
     if (done && last_workgroup(done, &s_last)) {
-#endif
         if (t < kRaw) cnt::fin_load<true>(gacc, raw, t);
         __syncthreads();
         cnt::fin_store(gacc, raw, out, t, blockDim.x);
@@ -145,7 +105,7 @@ hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nc
     const int64_t nblk = nchunks * chunk_len / 64;
     if (nblk <= 0 && parts == PART_ALL) return hipMemsetAsync(out, 0, 124 * sizeof(int64_t), s);
     if ((parts & PART_ACC) && nblk > 0) {
-        int grid = CNT_GRID;
+        int grid = kCntGrid;
         if ((int64_t)grid * kCountThreads > nblk)
             grid = (int)((nblk + kCountThreads - 1) / kCountThreads);
         // the whole call in one launch: its last workgroup finalizes

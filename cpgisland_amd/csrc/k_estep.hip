@@ -31,12 +31,7 @@
 // The E-step is a tolerance-bound fp64 computation (unlike the bit-exact Viterbi): products
 // and sums may be contracted to FMAs here (the fixed-point conversion of a posterior becomes
 // one fma(x, rz, 1.5*2^52): a single rounding onto the integer grid).
-#ifndef EST_CONTRACT
-#define EST_CONTRACT 1
-#endif
-#if EST_CONTRACT
 #pragma clang fp contract(fast)
-#endif
 
 namespace cpg {
 namespace {
@@ -47,10 +42,7 @@ constexpr int kSlab = 73;               // trans[64] (by dinucleotide x 4) | ini
 // workgroups add into kAccRep replicated accumulator sets (chosen by chunk index) so that
 // ~700 workgroups do not serialise on 73 device-scope atomic addresses; the finalize sums
 // the replicas in 128-bit integer arithmetic (exact, order-independent)
-#ifndef EST_ACC_REP
-#define EST_ACC_REP 16
-#endif
-constexpr int kAccRep = EST_ACC_REP;
+constexpr int kAccRep = 16;
 // xi bins: ONE set of 64 rows (k = pair, d = class: row k * 16 + d) x 16 columns (u64), lane
 // column = lane % 16.  An LDS 64-bit access serves 16 lanes per cycle with bank = (address /
 // 4) mod 32: the 16 lanes of a pass always hit 16 different columns = 32 different banks,
@@ -58,34 +50,8 @@ constexpr int kAccRep = EST_ACC_REP;
 // (per-wave replicated sets, measured earlier, collide whenever two lanes of a pass share a
 // class).
 // LDS: TA/TB (512 B) | union { 4-step tables, scan buffer, bins } | per-wave partials
-#ifndef EST_STATIC_T
-#define EST_STATIC_T 0
-#endif
-#ifndef EST_PRIO
-#define EST_PRIO 0
-#endif
-#ifndef EST_INIT_AFTER
-#define EST_INIT_AFTER 0
-#endif
-#if EST_STATIC_T
-// TA/TB as a static LDS array: its offset is known when the kernel is compiled, so a table
-// row's address is the code times 16 with the base in the instruction's offset field (one
-// add fewer per forward position than with the dynamic array's base)
-constexpr size_t kUnionOff = 0;
-#else
 constexpr size_t kUnionOff = 32 * 16;
-#endif
-#ifndef EST_TAB_IN_CKPT
-#define EST_TAB_IN_CKPT 0
-#endif
-#if EST_TAB_IN_CKPT
-// the 4-step tables (phase 1) live in the alpha-checkpoint region, which is written only
-// after the scans: the union holds just the scan buffer and the xi bins (8 KB), 24 KB less LDS
-// per workgroup for decode workgroups on the same CU
-constexpr size_t kUnionBytes = 64 * 16 * 8;
-#else
 constexpr size_t kUnionBytes = 2048 * 16;
-#endif
 __device__ __forceinline__ int bin_of(int d, int k) { return k * 16 + d; }
 
 struct Mat {
@@ -300,67 +266,40 @@ template <bool kAgent>
 __device__ void finalize(unsigned long long* acc, double* vsum, double* out);
 __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 
-#ifdef CPG_DEBUG_ESTEP
-#define CPG_EST_MARK(n) const unsigned long long n = wall_clock64();
-#else
-#define CPG_EST_MARK(n)
-#endif
 // waves per SIMD: the workgroup's 16 waves take 4 per SIMD; with <= 96 VGPRs (5 per SIMD) a
 // fifth wave slot and 128 VGPRs per SIMD stay free for the decode stream's kernels, whose
 // latency-bound waves then fill this kernel's idle issue slots (overlapped bench +3-4 %,
 // tools/ab_libs.sh; a few spills, none of them in the main loop's steady state).  At 4 per
 // SIMD (122 VGPRs, no spills) the kernel alone is as fast; 6 per SIMD spills 38.
-#ifndef EST_BLDS
-#define EST_BLDS 0
-#endif
-#ifndef EST_FPF
-#define EST_FPF 0   // forward table rows (LDS) read this many positions ahead (0: at use)
-#endif
-#ifndef CPG_EST_WPE
-#define CPG_EST_WPE 5
-#endif
+constexpr int kWavesPerEU = 5;
 // kCnt: the fused training pass — each lane also counts its 64 bases' labelled transitions
 // (count_dev.h; sign = the label bits), added into the count accumulators cacc, and the last
 // workgroup finalizes both (cout: cpg_counts_i64).  Needs >= 256 lanes (chunks >= 16 Ki).
 template <bool kCnt>
-__global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(CPG_EST_WPE)))
+__global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(kWavesPerEU)))
 void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
                    unsigned long long* __restrict__ acc, const double2* __restrict__ gtab,
                    unsigned int* done, double* __restrict__ out,
                    const uint32_t* __restrict__ sign, unsigned long long* __restrict__ cacc,
                    int64_t* __restrict__ cout) {
-#if EST_PRIO   // measurement knob: the E-step's waves raise their issue priority
-    __builtin_amdgcn_s_setprio(EST_PRIO);
-#endif
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves
     // conflict-free constant tables: 16 x 16 B each = one 256-B bank row
-#if EST_STATIC_T
-    __shared__ __attribute__((aligned(256))) double2 sTAB[32];
-    double2* TA = sTAB;                                       // (M(+,+), M(+,-))
-    double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
-    double2* TA4 = reinterpret_cast<double2*>(smem);          // 4-step products, row 0
-#else
     double2* TA = reinterpret_cast<double2*>(smem);          // (M(+,+), M(+,-))
     double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
     // one union region after TA/TB, used in turn by: the 4-step tables (phase 1), the scan
     // buffer (phase 2), the xi bins (phase 3) — each phase ends with a barrier
     double2* TA4 = TB + 16;                                   // 4-step products, row 0
-#endif
     auto* part = reinterpret_cast<unsigned long long*>(
         smem + kUnionOff + kUnionBytes);
     double2* fck = reinterpret_cast<double2*>(part + 16 * 64);   // [NMB][nl] alpha checkpoints
     unsigned char* uni = smem + kUnionOff;   // scan buffer (phase 2), xi bins (phase 3)
-#if EST_TAB_IN_CKPT
-    TA4 = fck;
-#endif
     double2* TB4 = TA4 + 1024;                                //                  row 1
     auto* bins = reinterpret_cast<unsigned long long*>(uni);  // [64 rows][16 columns]
     const int t = threadIdx.x;
     const int lane = t & 63;
     const int64_t c = blockIdx.x;
-    CPG_EST_MARK(T0)
     const uint32_t* pk = packed + c * (C / 16);
     // the one-step rows from the model's cached table (est_tables: L2-resident, 512 B)
     // rather than per-lane reads of the kernel-argument model
@@ -381,14 +320,10 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     if (kCnt) {   // the lane's 64 bases = one count block (its first is the chunk's first)
         __builtin_amdgcn_sched_barrier(0);   // kept apart from phase 1: registers
         if (t == 0) atomicAdd(&scnt[64 + cnt::init_state(cd0.raw[0], sg.x)], 1u);
-#ifndef CPG_FUSE_NOCOUNT   // measurement only: the sign loads without the counting
         cnt::Lane lc;
         lc.block(make_uint4(cd0.raw[0], cd0.raw[1], cd0.raw[2], cd0.raw[3]), sg, cd0.prev,
                  sgp >> 31, t == 0, scnt);
         lc.flush(scnt);
-#else
-        if (sg.x == 0x12345u && sgp == 7u) scnt[3] = 1u;
-#endif
         __builtin_amdgcn_sched_barrier(0);
     }
     // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4), from the rows
@@ -406,7 +341,6 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         TB4[i] = make_double2(x10, x11);
     }
     __syncthreads();
-    CPG_EST_MARK(T1)
 
     constexpr int L = kLanePos;            // 64 positions per lane
     constexpr int kMB = 16, NMB = L / kMB;
@@ -452,7 +386,6 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         P = mmul(P, G);   // normalised
         if (g < NMB - 1) Pk[g] = make_double4(P.a, P.b, P.c, P.d);
     }
-    CPG_EST_MARK(T2)
     // 2. prefix and suffix products of the lane products: shuffle scans inside each wave
     //    (interleaved), one wave scans the wave totals, two barriers in all
     const int wv = t >> 6;
@@ -530,7 +463,6 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         bM = B.c + B.d;
     }
     vnorm(bP, bM);
-    CPG_EST_MARK(T3)
     // the alpha checkpoints (see 3a) of every mini-block in LDS ([m][lane], 16 B: a wave's
     // row is conflict-free per 8-lane pass); mini-block 0's is (aP, aM) itself (no register
     // stays live across the main loop for it)
@@ -543,22 +475,17 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     }
     fck[t] = make_double2(aP, aM);
     __syncthreads();
-    CPG_EST_MARK(T4)
 
     // 3a. bins (aliasing the scan buffer, read above) zeroed; alpha entering mini-block m
     //     = alpha entering the lane times phase 1's product of the first m mini-blocks
     //     (any per-position scale cancels in the normalised xi)
     for (int i = t; i < 64 * 16; i += nl) bins[i] = 0ull;
     __syncthreads();
-    CPG_EST_MARK(T5)
     // 3b. mini-blocks, last to first: forward alphas in registers from the checkpoint, then
     //     backward with xi accumulation; beta flows on from one mini-block to the previous
     unsigned long long* wb = bins + (lane & 15);
     constexpr int kBS = 16;   // row stride
     double yP = bP, yM = bM;   // beta at the last position of the mini-block
-#ifdef CPG_STAMP_ESTEP
-    unsigned long long st_f1 = 0, st_b1 = 0, st_f2 = 0, st_b2 = 0;
-#endif
     // (measured and dropped: mini-block m's backward pass interleaved with mini-block m-1's
     // forward pass, two dependency chains per wave — 16 alpha pairs live either way, but the
     // two chains' temporaries spill: 0.18 vs 0.127 ms)
@@ -574,41 +501,18 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         // alpha registers hold one half of the mini-block: the second half's alphas from a
         // forward pass over all 16 positions, then (after its backward pass) the first half's
         // from a second forward pass — 32 fewer VGPRs than the whole mini-block's, for 2 extra
-        // fp64 per position, so that the kernel fits 5 waves per SIMD (see CPG_EST_WPE)
+        // fp64 per position, so that the kernel fits 5 waves per SIMD (see kWavesPerEU)
         constexpr int kH = kMB / 2;
         double alP[kH], alM[kH];
         double hP = bfP, hM = bfM;   // alpha at position lo - 1 (the position before the half)
         int kf[kMB / 4];   // alpha's power-of-two shifts at positions 3, 7, 11, 15
         auto forward = [&](int lo, int hi) {   // positions [0, hi); alphas of [lo, hi) kept
             double xP = bfP, xM = bfM;
-#if EST_FPF
-            // the table rows of position i + EST_FPF issued before position i's products:
-            // the rows depend only on the codes, so the LDS latency leaves the alpha chain
-            double2 fa[EST_FPF + 1], fb[EST_FPF + 1];
-#pragma unroll
-            for (int j = 0; j < EST_FPF; ++j) {
-                const uint32_t d = code_at(cm, j);
-                fa[j] = TA[d];
-                fb[j] = TB[d];
-            }
-#endif
 #pragma unroll
             for (int i = 0; i < hi; ++i) {
-#if EST_FPF
-                if (i + EST_FPF < hi) {
-                    const uint32_t d = code_at(cm, i + EST_FPF);
-                    fa[(i + EST_FPF) % (EST_FPF + 1)] = TA[d];
-                    fb[(i + EST_FPF) % (EST_FPF + 1)] = TB[d];
-                }
-                __builtin_amdgcn_sched_barrier(0);
-#endif
                 if (!(t == 0 && m == 0 && i == 0)) {   // (alpha_0 itself at the chunk start)
-#if EST_FPF
-                    const double2 ma = fa[i % (EST_FPF + 1)], mb = fb[i % (EST_FPF + 1)];
-#else
                     const uint32_t d = code_at(cm, i);
                     const double2 ma = TA[d], mb = TB[d];
-#endif
                     const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
                     xP = nP;
                     xM = nM;
@@ -639,43 +543,33 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
             yP *= r;
             yM *= r;
         };
-#ifndef EST_PFD
-#define EST_PFD 1   // backward table rows loaded this many positions ahead (2, 3: no faster)
-#endif
+constexpr int kPFD = 1;   // backward table rows loaded this many positions ahead (2, 3: no faster)
         // the backward pass's table rows come from a global copy (L1-resident): waited on
         // with vmcnt, not behind the preceding LDS atomics (LDS operations retire in order;
         // an LDS copy read ahead of the atomics spills)
         auto backward = [&](int lo, int hi) {   // positions hi - 1 .. lo
-            double2 qa[EST_PFD + 1], qb[EST_PFD + 1];
+            double2 qa[kPFD + 1], qb[kPFD + 1];
             auto trow = [&](int i, double2& a, double2& b) {
                 const uint32_t d = code_at(cm, i);
-#if EST_BLDS   // measurement: the rows from the LDS copy (issued ahead of the atomics)
-                a = TA[d];
-                b = TB[d];
-#else
                 a = gtab[d];
                 b = gtab[16 + d];
-#endif
             };
 #pragma unroll
-            for (int j = 0; j < EST_PFD; ++j) trow(hi - 1 - j, qa[j], qb[j]);
+            for (int j = 0; j < kPFD; ++j) trow(hi - 1 - j, qa[j], qb[j]);
 #pragma unroll
             for (int i = hi - 1; i >= lo; --i) {
-                // table rows issued EST_PFD positions ahead; the scheduling barrier keeps the
+                // table rows issued kPFD positions ahead; the scheduling barrier keeps the
                 // compiler from sinking them to their use, which had put one full L1/L2 round
                 // trip (two, serialised) on every position's chain
-                if (i - EST_PFD >= lo)
-                    trow(i - EST_PFD, qa[(hi - 1 - i + EST_PFD) % (EST_PFD + 1)],
-                         qb[(hi - 1 - i + EST_PFD) % (EST_PFD + 1)]);
+                if (i - kPFD >= lo)
+                    trow(i - kPFD, qa[(hi - 1 - i + kPFD) % (kPFD + 1)],
+                         qb[(hi - 1 - i + kPFD) % (kPFD + 1)]);
                 __builtin_amdgcn_sched_barrier(0);
                 const uint32_t d = code_at(cm, i);
-                const double2 ma = qa[(hi - 1 - i) % (EST_PFD + 1)],
-                              mb = qb[(hi - 1 - i) % (EST_PFD + 1)];
+                const double2 ma = qa[(hi - 1 - i) % (kPFD + 1)],
+                              mb = qb[(hi - 1 - i) % (kPFD + 1)];
                 if (t == 0 && m == 0 && i == 0) {   // gamma_0 = a_0 * y_0 / 2^47 -> init counts,
                     // added at once (nothing stays live across the main loop for it)
-#if EST_INIT_AFTER   // (after the loop: no global atomics in the loop body)
-                    continue;
-#endif
                     const uint32_t b0 = pk[0] & 3u;
                     unsigned long long* ra = acc + 2 * kSlab * (c % kAccRep);
                     acc128_add(ra + 2 * (64 + b0), to_fixed_scaled(alP[0] * yP), false);
@@ -689,9 +583,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
                 atomicAdd(wb + bin_of(d, 0) * kBS, raw_fma(uP, t00));
                 atomicAdd(wb + bin_of(d, 1) * kBS, raw_fma(uP, t01));
                 atomicAdd(wb + bin_of(d, 2) * kBS, raw_fma(uM, t10));
-#ifndef EST_DROP4   // measurement only: without the 4th bin's atomic (wrong results)
                 atomicAdd(wb + bin_of(d, 3) * kBS, raw_fma(uM, t11));
-#endif
                 yP = t00 + t01;
                 yM = t10 + t11;
                 if (i == 4 || i == 8 || i == 12) {
@@ -700,50 +592,13 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
                 }
             }
         };
-#if defined(CPG_STAMP_ESTEP)   // diagnostic build: shader-clock cycles per pass
-
-#define EST_STAMP(v)                                                                   \
-    __builtin_amdgcn_sched_barrier(0);                                                 \
-    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(v)::"memory");          \
-    __builtin_amdgcn_sched_barrier(0);
-        unsigned long long s0, s1, s2, s3, s4;
-        EST_STAMP(s0)
-        forward(kH, kMB);
-        EST_STAMP(s1)
-        bstart();
-        backward(kH, kMB);
-        EST_STAMP(s2)
-        forward(0, kH);
-        EST_STAMP(s3)
-        backward(0, kH);
-        EST_STAMP(s4)
-        st_f1 += s1 - s0;
-        st_b1 += s2 - s1;
-        st_f2 += s3 - s2;
-        st_b2 += s4 - s3;
-#else
         forward(kH, kMB);
         bstart();
         backward(kH, kMB);
         forward(0, kH);
         backward(0, kH);
-#endif
     }
-#if EST_INIT_AFTER
-    if (t == 0) {   // lane 0 ends at position 0: y = y_0 (its update was skipped), a_0 = fck[0]
-        const double2 a0 = fck[0];
-        const uint32_t b0 = pk[0] & 3u;
-        acc128_add(racc + 2 * (64 + b0), to_fixed_scaled(a0.x * yP), false);
-        acc128_add(racc + 2 * (64 + b0 + 4), to_fixed_scaled(a0.y * yM), false);
-    }
-#endif
-#ifdef CPG_STAMP_ESTEP
-    if (lane == 0 && (c == 0 || c == 300 || c == 700) && (t >> 6) % 5 == 0)
-        printf("stamp c%lld w%d: fwd16 %llu bwd8 %llu fwd8 %llu bwd8 %llu (cycles, 4 mini-blocks)\n",
-               (long long)c, t >> 6, st_f1, st_b1, st_f2, st_b2);
-#endif
     __syncthreads();
-    CPG_EST_MARK(T6)
     // the epilogue's indices from an opaque copy of the thread index: the compiler would
     // otherwise keep the prologue's (shuffle) indices live across the main loop, in scratch
     int te = threadIdx.x;
@@ -757,7 +612,6 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         part[te] = s;
     }
     __syncthreads();
-    CPG_EST_MARK(T7)
     // chunk results -> the global 128-bit accumulators: xi bins and the init posteriors in
     // 2^-47 units, the log-likelihood in signed 2^-24 units
     if (te < 64) {   // row te = d * 4 + k (wave 0)
@@ -782,12 +636,6 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         if (kCnt) cnt::fin_store(cacc, craw, cout, te, nl);
         reset_done(done);
     }
-#ifdef CPG_DEBUG_ESTEP
-    if (t == 0 && (c == 0 || c == 300 || c == (int64_t)gridDim.x - 1))
-        printf("estep c%lld: tables %llu product %llu scans %llu ckpt %llu zero %llu main %llu "
-               "binsum %llu (wall-clock ticks, 100 MHz)\n", (long long)c, T1 - T0, T2 - T1,
-               T3 - T2, T4 - T3, T5 - T4, T6 - T5, T7 - T6);
-#endif
 }
 
 
@@ -858,14 +706,9 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
 size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep + 1024; }
 
 namespace {
-#ifndef CPG_EST_LDS_PAD
-#define CPG_EST_LDS_PAD 0   // measurement only: extra LDS per workgroup (co-residency probe)
-#endif
 size_t estep_lds(int lanes) {   // the union is sized for 16 waves; fewer lanes use a prefix
     const size_t ck = (size_t)(kLanePos / 16) * lanes * sizeof(double2);
-    return kUnionOff + kUnionBytes + 16 * 64 * sizeof(unsigned long long) +
-           (EST_TAB_IN_CKPT ? std::max(ck, (size_t)2048 * sizeof(double2)) : ck) +
-           CPG_EST_LDS_PAD;
+    return kUnionOff + kUnionBytes + 16 * 64 * sizeof(unsigned long long) + ck;
 }
 }  // namespace
 

@@ -31,21 +31,12 @@
 
 #include "cpg_internal.h"
 
-#ifndef ING_POLL
-#define ING_POLL 0
-#endif
-#ifndef ING_ABL
-#define ING_ABL 0   // development ablations (tools/build_ablations.sh); 0 in the product
-#endif
 
 namespace cpg {
 namespace {
 
 constexpr int kIT = 256;                       // lanes per tile
-#ifndef ING_ROWS
-#define ING_ROWS 8
-#endif
-constexpr int kIRows = ING_ROWS;               // rows of 1 KiB per wave (8: 32 KiB tiles)
+constexpr int kIRows = 8;                      // rows of 1 KiB per wave (8: 32 KiB tiles)
 constexpr int kTileBytes = kIT * 16 * kIRows;  // <= 32 KiB: one residue point per tile
 static_assert(kIRows % 2 == 0 && kTileBytes <= 32768, "2..8 rows of 1 KiB per wave");
 constexpr int kTileWords = kTileBytes / 16;    // packed words for a tile of valid bytes
@@ -70,11 +61,7 @@ __device__ __forceinline__ void gstore(unsigned long long* p, unsigned long long
     __hip_atomic_store((gu64*)p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 __device__ __forceinline__ unsigned long long gload(const unsigned long long* p) {
-#if ING_POLL == 1   // poll with a returning RMW (performed at the device coherence point)
-    return __hip_atomic_fetch_or((gu64*)p, 0ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#else
     return __hip_atomic_load((gu64*)p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-#endif
 }
 
 // Exclusive prefix of the granules before `tile` (one wave, uniform).  Each pass reads a
@@ -82,13 +69,7 @@ __device__ __forceinline__ unsigned long long gload(const unsigned long long* p)
 // granules up to the nearest inclusive one.  Wide windows matter: every tile of a dispatch
 // round publishes its aggregate at about the same time, so the nearest inclusive granule is
 // typically a round (~2,000 tiles) back, and each pass costs one device-scope round trip.
-#ifndef ING_SLEEP
-#define ING_SLEEP 1
-#endif
-#ifndef ING_LBW
-#define ING_LBW 1
-#endif
-constexpr int kLbw = ING_LBW;
+constexpr int kLbw = 1;   // wider windows were slower (polling traffic)
 __device__ unsigned long long lookback(const unsigned long long* st, long long tile, int lane,
                                        unsigned int* timeout) {
     unsigned long long excl = 0;
@@ -121,7 +102,7 @@ __device__ unsigned long long lookback(const unsigned long long* st, long long t
                 if (lane == 0) atomicOr(timeout, 1u);
                 return excl;
             }
-            __builtin_amdgcn_s_sleep(ING_SLEEP);
+            __builtin_amdgcn_s_sleep(1);
         }
         unsigned long long v = 0;
 #pragma unroll
@@ -275,11 +256,7 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
             if (lane == 0) gstore(ws.stV, kFlagInc | agg);
         } else {
             if (lane == 0) gstore(ws.stV + tile, kFlagAgg | agg);
-#if ING_ABL == 1   // development ablation: no look-back (wrong offsets, timing only)
-            vex = (unsigned long long)tile * 16000ull;
-#else
             vex = lookback(ws.stV, tile, lane, ws.timeout);
-#endif
             if (lane == 0) gstore(ws.stV + tile, kFlagInc | ((vex + agg) & kValMask));
         }
         if (lane == 0) s_vex = vex;
@@ -340,11 +317,7 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
                 if (lane == 0) gstore(ws.stQ, kFlagInc | (unsigned)qt);
             } else {
                 if (lane == 0) gstore(ws.stQ + tile, kFlagAgg | (unsigned)qt);
-#if ING_ABL == 1
-                qp = 0;
-#else
                 qp = lookback(ws.stQ, tile, lane, ws.timeout);
-#endif
                 if (lane == 0) gstore(ws.stQ + tile, kFlagInc | (qp + (unsigned)qt));
             }
             if (lane == 0) s_qp = qp;
@@ -383,7 +356,7 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
     const long long P = (long long)vex + (long long)qp * C;
     const bool gap = qchain && qt > 0;
     const long long lenA = gap ? (ls < (long long)agg ? ls : (long long)agg) : (long long)agg;
-    for (int run = 0; run < (ING_ABL == 2 ? 0 : 2); ++run) {
+    for (int run = 0; run < 2; ++run) {
         const long long s0 = run == 0 ? 0 : lenA;
         const long long len = run == 0 ? lenA : (gap ? (long long)agg - lenA : 0);
         if (len <= 0) continue;

@@ -34,10 +34,7 @@ namespace {
 
 constexpr int kIT = 1024;    // lanes of the per-chunk kernels
 constexpr int kTT = 256;     // lanes of the tile kernel
-#ifndef ISL_TROWS
-#define ISL_TROWS 1
-#endif
-constexpr int kTRows = ISL_TROWS;   // rows of kTT * 4 words per tile (1: 1,376 tiles per
+constexpr int kTRows = 1;           // rows of kTT * 4 words per tile (1: 1,376 tiles per
                                     // 46 Mbp — 7.3 us; 4 rows: 344 tiles — 11.0 us)
 constexpr int64_t kTW = (int64_t)kTT * 4 * kTRows;   // words per tile (1,024 with one row)
 // a fused decode's tiles: one traceback workgroup's 256 blocks of 256 positions

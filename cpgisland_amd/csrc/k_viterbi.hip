@@ -286,66 +286,13 @@ __device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
     return reinterpret_cast<const VitDerived*>(vt + 1);
 }
 
-// measurement knob: extra static LDS per workgroup of K1 / K3 / K7 (bytes), so that those
-// kernels cannot share a CU with the E-step (co-residency probe)
-#define VIT_LDS_PAD(n)                                                                     \
-    __shared__ volatile unsigned char vit_pad_[(n) > 0 ? (n) : 1];                          \
-    {                                                                                      \
-        int z_ = threadIdx.x;                                                              \
-        asm volatile("" : "+v"(z_));                                                       \
-        if (z_ == 0x7fffffff) vit_pad_[z_ & 1] = 0;                                        \
-    }
-#ifndef VIT_PAD_K1
-#define VIT_PAD_K1 0
-#endif
-#ifndef VIT_PAD_K3
-#define VIT_PAD_K3 0
-#endif
-#ifndef VIT_PAD_K7
-#define VIT_PAD_K7 0
-#endif
-// measurement knob: decode waves raise their issue priority (s_setprio) over the co-resident
-// E-step waves, which the SIMD's oldest-first arbitration otherwise favours
-#ifndef VIT_PRIO
-#define VIT_PRIO 0
-#endif
-#if VIT_PRIO
-#define VIT_PRIO_RAISE() __builtin_amdgcn_s_setprio(VIT_PRIO)
-#else
-#define VIT_PRIO_RAISE() ((void)0)
-#endif
 // Waves per SIMD a kernel is compiled for (VGPR budget 512 / n).  On a training CU the
 // E-step holds 4 waves x 96 VGPRs per SIMD, leaving 128: a decode kernel of <= 64 VGPRs gets
 // two wave slots there instead of one.  K5 (the longest decode kernel under overlap) is built
 // for 8 (64 VGPRs; its few spills are outside the step loop): bench +2 % with the 2-deep
 // lookup ring below (profiles/r02_v10/ab_k5_occupancy*.log).  K3 at 8 (spills) and K7 at 8 (75
-// spills) were slower; K1 cannot reach 64.  The others stay measurement knobs.
-#ifndef VIT_K5_WPE
-#define VIT_K5_WPE 8
-#endif
-#ifndef VIT_K1_SLIM
-#define VIT_K1_SLIM 0
-#endif
-#ifdef VIT_K1_WPE
-#define K1_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K1_WPE)))
-#else
-#define K1_ATTR
-#endif
-#ifdef VIT_K3_WPE
-#define K3_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K3_WPE)))
-#else
-#define K3_ATTR
-#endif
-#ifdef VIT_K5_WPE
-#define K5_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K5_WPE)))
-#else
-#define K5_ATTR
-#endif
-#ifdef VIT_K7_WPE
-#define K7_ATTR __attribute__((amdgpu_waves_per_eu(VIT_K7_WPE)))
-#else
-#define K7_ATTR
-#endif
+// spills) were slower; K1 cannot reach 64 at its LDS (the slim-LDS variant at 64 lost 1.5 %).
+constexpr int kK5WavesPerEU = 8;
 __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables* vt) {
     VitDerived* dv = reinterpret_cast<VitDerived*>(vt + 1);
     const int n = kQ4 + kMaxBinade * 16 + kMaxBinade * 64 + kMaxBinade * kW4;
@@ -416,36 +363,20 @@ __device__ __forceinline__ int64_t fix_of(double x, int f);
 __device__ __forceinline__ VitPlan classify(const VitConsts& vc, const Geo& g, int64_t k,
                                             longlong2 en, longlong2 ex, bool& irregular);
 
-__global__ __launch_bounds__(kThreads) K1_ATTR void k_vit_approx(VitConsts vc, const uint32_t* packed,
+__global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uint32_t* packed,
                                                          Geo g, const VitTables* vt,
                                                          int4* __restrict__ comp, ApproxSeg as) {
-    VIT_PRIO_RAISE();
-#if VIT_PAD_K1
-    VIT_LDS_PAD(VIT_PAD_K1)
-#endif
     __shared__ int4 Q[16];
     // 4-step products over 5-base windows b0..b4 (exact: integers) [0, 1024), then the
     // 3-step products of steps 1..3 over b1..b4 [1024, 1280): block 0's first window (the
     // chunk's position 0 carries no step) — copied from the per-model tables (k_vit_tables)
-#if VIT_K1_SLIM
-    // only the 4-step entries in LDS (16 KB: eight 256-lane
-    // workgroups per CU, so that the compiler may budget 64 VGPRs); block 0's 3-step first
-    // window comes from the global table into the accumulator
-    __shared__ int4 Q4[1024];
-#else
     __shared__ int4 Q4[kQ4];
-#endif
     if (threadIdx.x < 16)
         Q[threadIdx.x] = make_int4(vc.Q[threadIdx.x][0], vc.Q[threadIdx.x][1],
                                    vc.Q[threadIdx.x][2], vc.Q[threadIdx.x][3]);
     const int4* gq = derived(vt)->Q4;
-#if VIT_K1_SLIM
-#pragma unroll
-    for (int i = 0; i < 1024 / kThreads; ++i) Q4[threadIdx.x + i * kThreads] = gq[threadIdx.x + i * kThreads];
-#else
 #pragma unroll
     for (int i = 0; i < kQ4 / kThreads; ++i) Q4[threadIdx.x + i * kThreads] = gq[threadIdx.x + i * kThreads];
-#endif
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;   // (segment path: every lane is valid)
@@ -455,32 +386,15 @@ __global__ __launch_bounds__(kThreads) K1_ATTR void k_vit_approx(VitConsts vc, c
         int4 acc = make_int4(0, kNeg32, kNeg32, 0);
         const BlockWords bw = load_block(pk, k);
         const bool first = k == 0;
-#if VIT_K1_SLIM
-        // block 0's first window (3 steps: position 0 carries none) from the global table,
-        // multiplied in the same order as the other windows; its ring slot is skipped below
-        if (first) acc = i4_mul(acc, gq[1024u + (((bw.w[0] << 2) & 0x3FFu) >> 2)]);
-#endif
-#ifndef VIT_K1_LOOK
-#define VIT_K1_LOOK 4
-#endif
-        pipelined<VIT_K1_LOOK, 64>(
+        pipelined<4, 64>(
             [&](int j) {   // 5-base window of steps 4j .. 4j+3
                 const int r = j >> 2, s = j & 3;
                 const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
                 const uint32_t wi = s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 0x3FFu)
                                            : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
-#if VIT_K1_SLIM
-                return wi;
-#else
                 return (j == 0 && first) ? 1024u + (wi >> 2) : wi;
-#endif
             },
-#if VIT_K1_SLIM
-            [&](uint32_t wi) { return Q4[wi]; },
-            [&](const int4 q, int j) { if (j != 0 || !first) acc = i4_mul(acc, q); });
-#else
             [&](uint32_t wi) { return Q4[wi]; }, [&](const int4 q, int) { acc = i4_mul(acc, q); });
-#endif
         if (as.agg) {   // segment path (whole blocks only)
             approx_segment(vc, g, pk, c, k, CI{acc.x, acc.y, acc.z, acc.w}, as);
             return;
@@ -755,7 +669,7 @@ __device__ __forceinline__ C64 shfl_up_c64(const C64& x, int d) {
     return {__shfl_up(x.pp, d), __shfl_up(x.pm, d), __shfl_up(x.mp, d), __shfl_up(x.mm, d)};
 }
 
-__global__ __launch_bounds__(kThreads) K3_ATTR void k_vit_exact(VitConsts vc, const VitTables* vt,
+__global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitTables* vt,
                                                         const uint32_t* packed, Geo g,
                                                         VitPlan* __restrict__ plan,
                                                         double4* __restrict__ comp3,
@@ -767,10 +681,6 @@ __global__ __launch_bounds__(kThreads) K3_ATTR void k_vit_exact(VitConsts vc, co
                                                         SegSum* __restrict__ seg,
                                                         const int32_t* __restrict__ irrseg,
                                                         double2* __restrict__ vhead) {
-    VIT_PRIO_RAISE();
-#if VIT_PAD_K3
-    VIT_LDS_PAD(VIT_PAD_K3)
-#endif
     // per binade slot: single-step halves sA/sB [16] (one 256-B bank row each) and 2-step
     // composites over 3-base windows, halves P2A = (pp, pm), P2B = (mp, mm) [64].  Every
     // entry is a sum of binade-rounded constants: exact on the binade's grid.
@@ -1154,11 +1064,6 @@ __device__ __forceinline__ double2 chain_window(const uint32_t* __restrict__ pk,
     return make_double2(__shfl(P, 0), __shfl(M, 0));
 }
 
-#ifdef CPG_DEBUG_CHAIN
-#define CPG_CHAIN_MARK(n) const unsigned long long n = wall_clock64();
-#else
-#define CPG_CHAIN_MARK(n)
-#endif
 __global__ __launch_bounds__(kChainT) void k_vit_chain(
     VitConsts vc, const uint32_t* packed, Geo g, const VitPlan* __restrict__ plan,
     const double4* __restrict__ comp3, const uint8_t* __restrict__ degen,
@@ -1191,7 +1096,6 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
     // block 0's exit value (K2's head lanes), needed by the serial chain: read now, so that its
     // latency is not on the chain
     const double2 vhead0 = t == 0 ? vhead[c] : make_double2(0.0, 0.0);
-    CPG_CHAIN_MARK(T0)
     // phase 1: thread-local pieces.  A thread owns `per` (<= kPre for chunks up to 1 Mi)
     // consecutive blocks; their plans and composites are loaded up front, all in flight.
     constexpr int kPre = 4;
@@ -1259,7 +1163,6 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
             piece(k, pl[k], ld_c64(cp + k), ld_c64(cq + k));
     }
     if (!hasb) lead = run;
-    CPG_CHAIN_MARK(T1)
     // phase 2: segmented scan of (hasb, trail) + barrier count scan: shuffle scans inside
     // each wave, then the 16 wave totals (exact max-plus products: any association)
     struct Seg {
@@ -1282,10 +1185,8 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         if (lane >= d) x = seg_comb(y, x);
     }
     __shared__ Seg sWave[kChainT / 64];
-    CPG_CHAIN_MARK(T1a)
     if (lane == 63) sWave[wv] = x;
     __syncthreads();
-    CPG_CHAIN_MARK(T1b)
     Seg before{c64_id(), 0, 0};   // everything before this wave
     for (int w = 0; w < wv; ++w) before = seg_comb(before, sWave[w]);
     const Seg prev = seg_shfl_up(x, 1);   // inclusive value of the lane before
@@ -1328,9 +1229,7 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
             }
         }
     }
-    CPG_CHAIN_MARK(T1c)
     __syncthreads();
-    CPG_CHAIN_MARK(T2)
     // phase 3: the serial chain over barriers.  The whole workgroup first stages every
     // window's step constants and every gap composite in LDS, so lane 0's serial
     // recurrence never waits on global memory; windows beyond the staging capacity fall
@@ -1369,7 +1268,6 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         }
     }
     __syncthreads();
-    CPG_CHAIN_MARK(T3)
     const bool all_staged = nst == nbar && sWoff[nst] <= kStageSteps;
     if (all_staged) {
         // every window staged: lane 0 alone runs the chain (no per-window broadcasts); the
@@ -1447,7 +1345,6 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
         }
     }
     __syncthreads();
-    CPG_CHAIN_MARK(T4)
     // phase 4: entries
     double2 v = (bidx0 > 0) ? voc[bidx0 - 1] : init;
     if (t > 0) v = c64_apply(v, incoming);
@@ -1482,15 +1379,6 @@ __global__ __launch_bounds__(kChainT) void k_vit_chain(
             entries(k, pl[k], ld_c64(cp + k), ld_c64(cq + k));
     }
     if (b1 == g.nsb && b0 < b1) ent[g.nsb] = v;
-    CPG_CHAIN_MARK(T5)
-#ifdef CPG_DEBUG_CHAIN
-    if (t == 0 && (c == 0 || c == g.nchunks - 1))
-        printf("chain c%lld nbar %d steps %d staged %d: phase1 %llu scan %llu (shfl %llu bar1 %llu "
-               "combine+list %llu bar2 %llu) list+stage %llu serial %llu entries %llu "
-               "(wall-clock ticks)\n",
-               (long long)c, nbar, sWoff[nst], (int)all_staged, T1 - T0, T2 - T1, T1a - T1,
-               T1b - T1a, T1c - T1b, T2 - T1c, T3 - T2, T4 - T3, T5 - T4);
-#endif
 }
 
 // K4, segment path (one 256-lane workgroup per chunk of 16 segments): the barrier list from
@@ -1506,7 +1394,6 @@ __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
     const double4* __restrict__ rx, const SegSum* __restrict__ seg, double2* __restrict__ entry,
     double2* __restrict__ went, double4* __restrict__ gap, int32_t* __restrict__ barlist,
     double2* __restrict__ vout, const double2* __restrict__ vhead) {
-    VIT_PRIO_RAISE();
     const int64_t c = blockIdx.x;
     const int t = threadIdx.x;
     const int nseg = (int)(g.nsb / kThreads);
@@ -1831,10 +1718,7 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
     if (g.whole(k)) {
         // quads of 64 steps; the ring of kLook lookups in flight runs across quad borders
         // (2 deep: at the 64-VGPR budget, 4 had spilled more and measured slower)
-#ifndef VIT_K5_LOOK
-#define VIT_K5_LOOK 2
-#endif
-        constexpr int kLook = VIT_K5_LOOK;
+        constexpr int kLook = 2;
         auto fetch = [&](uint32_t d) { return C64{LA[d].x, LA[d].y, LB[d].x, LB[d].y}; };
         auto code = [](const uint4 w, uint32_t prev, int j) {   // j compile-time, < 64
             const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
@@ -2004,7 +1888,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
 // that workgroup); the origin maps then cross workgroups inside the kernel, 4 per
 // agent-scope atomic word.
 template <bool kScan>
-__global__ __launch_bounds__(kThreads) K5_ATTR void k_vit_forward(VitConsts vc, const uint32_t* packed,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kK5WavesPerEU))) void k_vit_forward(VitConsts vc, const uint32_t* packed,
                                                           Geo g, const uint8_t* __restrict__ degen,
                                                           const double2* __restrict__ entry,
                                                           uint4* __restrict__ bp,
@@ -2016,7 +1900,6 @@ __global__ __launch_bounds__(kThreads) K5_ATTR void k_vit_forward(VitConsts vc, 
                                                           unsigned int* done,
                                                           uint8_t* __restrict__ endst,
                                                           double* __restrict__ score) {
-    VIT_PRIO_RAISE();
     // conflict-free halves (16 x 16 B each); entry 16 is the identity step (0, -inf, -inf,
     // 0) standing for block 0's position 0: P + 0.0 = P and M + -inf = -inf exactly, so the
     // values, the tie bits that matter and the origins are unchanged by it
@@ -2118,17 +2001,13 @@ __device__ __forceinline__ void trace_tile(const uint32_t (&out)[8], const uint3
 }
 
 template <bool kIsl>
-__global__ __launch_bounds__(kThreads) K7_ATTR void k_vit_trace(Geo g, const uint4* __restrict__ bp,
+__global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __restrict__ bp,
                                                         const uint8_t* __restrict__ endst,
                                                         uint32_t* __restrict__ sign_out,
                                                         uint32_t* status, uint32_t* zero_at,
                                                         int64_t zero_n,
                                                         const uint32_t* __restrict__ packed,
                                                         IslFuse fz) {
-    VIT_PRIO_RAISE();
-#if VIT_PAD_K7
-    VIT_LDS_PAD(VIT_PAD_K7)
-#endif
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     // the undecoded tail's sign words ('-'), in this launch rather than a memset of its own
     for (int64_t i = gid; i < zero_n; i += (int64_t)gridDim.x * kThreads) zero_at[i] = 0u;
