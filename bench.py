@@ -286,16 +286,20 @@ def main():
     nlanes = 1 if (args.serial or args.no_overlap) else max(1, args.lanes)
     icap = 1 << 20
 
+    ntl = 1 if (args.serial or args.no_overlap) else max(1, args.train_lanes)
+    nrec = ntl if ntl >= 2 else 2
+
     def make_lane(cx):
         # the training pass writes one rank record per step (E-step doubles | labelled-count
-        # int64: cpgisland_amd/dist.py train_record), double-buffered so that step k+1's
-        # training pass does not wait for step k's all-gather
-        recs = [cdist.train_record(dev) for _ in range(2)]
+        # int64: cpgisland_amd/dist.py train_record), one per training lane and at least two,
+        # so that step k+1's training pass does not wait for step k's all-gather and two
+        # training streams never write the same record
+        recs = [cdist.train_record(dev) for _ in range(nrec)]
         return {"ctx": cx, "recs": recs,
                 "gath": [torch.empty(world * cdist.TRAIN_RECORD, dtype=torch.float64, device=dev)
-                         for _ in range(2)],
-                "ev_tr": [torch.cuda.Event() for _ in range(2)],
-                "ev_red": [torch.cuda.Event() for _ in range(2)],
+                         for _ in range(nrec)],
+                "ev_tr": [torch.cuda.Event() for _ in range(nrec)],
+                "ev_red": [torch.cuda.Event() for _ in range(nrec)],
                 "emerged": torch.empty(105, dtype=torch.float64, device=dev),
                 "lmerged": torch.empty(124, dtype=torch.int64, device=dev),
                 "so": torch.empty(D.words32(N) + 4, dtype=torch.int32, device=dev),
@@ -367,7 +371,6 @@ def main():
             ln["parts"].append({"ctx": cx2, "s": torch.cuda.Stream(priority=-1 if args.prio else 0),
                                 "iout": torch.empty((icap, 32), dtype=torch.uint8, device=dev),
                                 "icnt": torch.zeros(1, dtype=torch.int64, device=dev)})
-    ntl = 1 if (args.serial or args.no_overlap) else max(1, args.train_lanes)
     ndl = 1 if (args.serial or args.no_overlap) else max(1, args.decode_lanes)
 
     def train_stream():
@@ -457,11 +460,11 @@ def main():
                         mark("islands", 1)
                     if probe and probe[0] == "dec":
                         torch.cuda._sleep(probe[1])
-        par = k & 1
+        par = k % nrec   # (training lane k % ntl writes record k % nrec: ntl divides nrec)
         rec, ecnt, lcnt = ln["recs"][par]
         cx, s_tr = ln["tr"][k % ntl]   # (the decode above ran on the lane's own context)
         with torch.cuda.stream(s_tr):
-            if dist and k >= 2:   # this record's previous all-gather has read it
+            if dist and k >= nrec:   # this record's previous all-gather has read it
                 s_tr.wait_event(ln["ev_red"][par])
             if fused:   # "estep" = the whole training pass (E-step + labelled counts)
                 mark("estep", 0)

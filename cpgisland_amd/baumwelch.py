@@ -39,10 +39,16 @@ def normalize_labelled(counts) -> HmmModel:
 
 
 def converged(old: HmmModel, new: HmmModel, epsilon: float) -> bool:
-    """Mahout HmmTrainer.checkConvergence: sqrt(sum (dA)^2) + sqrt(sum (dB)^2) < eps."""
-    na = math.sqrt(float(np.sum((old.a - new.a) ** 2)))
-    nb = math.sqrt(float(np.sum((old.b - new.b) ** 2)))
-    return na + nb < epsilon
+    """Mahout HmmTrainer.checkConvergence: sqrt(sum (dA)^2) + sqrt(sum (dB)^2) < eps, the sums
+    taken element by element in row-major order as the Java loops do (not numpy's pairwise
+    summation, which rounds differently)."""
+    def norm(x, y):
+        acc = 0.0
+        for u, v in zip(np.ravel(x).tolist(), np.ravel(y).tolist()):
+            d = u - v
+            acc += d * d
+        return math.sqrt(acc)
+    return norm(old.a, new.a) + norm(old.b, new.b) < epsilon
 
 
 def estep(ctx: Context, model: HmmModel, packed, nbases: int,

@@ -2,6 +2,7 @@
 // the HBM-resident "_d" entry points and the host-buffer wrappers that mirror the
 // reference call sites (CpGIslandFinder.java:200 training, :260 decode, :262-339 islands).
 
+#include <algorithm>
 #include <cstdlib>
 #include <cmath>
 #include <cstring>
@@ -198,13 +199,25 @@ int cpg_reserve(cpg_ctx* ctx, int64_t nbases) {
     CPG_HIP(hipSetDevice(ctx->device));
     void* p;
     int rc;
-    const int64_t nd = nbases / CPG_DECODE_CHUNK + 1, nt = nbases / CPG_TRAIN_CHUNK + 1;
+    // every slot at its largest over the chunk lengths the decode entry points take (multiples
+    // of 4096 up to the reference's 1 Mi): the per-chunk slots (look-back words, done counters)
+    // grow with the chunk count, so a reserve for 1 Mi chunks alone would still let a later call
+    // with shorter chunks grow a slot — a device-wide synchronisation (ws_get)
+    size_t vit = 0, isl = 0, agg = 0, per_chunk = 0;
+    for (int64_t C = 4096; C <= CPG_DECODE_CHUNK; C *= 2) {
+        const int64_t nd = nbases / C + 1;
+        vit = std::max(vit, viterbi_ws_bytes(nd, C));
+        isl = std::max(isl, islands_ws_bytes(nd, C));
+        agg = std::max(agg, viterbi_agg_bytes(nd, C));
+        per_chunk = std::max(per_chunk, (size_t)(nd + 1) * 8);
+    }
+    const int64_t nt = nbases / 4096 + 1;
     if ((rc = ws_get(ctx, WS_COUNT, count_ws_bytes(nt), &p))) return rc;
-    if ((rc = ws_get(ctx, WS_VIT, viterbi_ws_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
-    if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
-    if ((rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(nd, CPG_DECODE_CHUNK), &p))) return rc;
-    if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nd + 1) * 8, &p))) return rc;
-    if ((rc = ws_get(ctx, WS_IDONE, (size_t)(nd + 1) * 8, &p))) return rc;
+    if ((rc = ws_get(ctx, WS_VIT, vit, &p))) return rc;
+    if ((rc = ws_get(ctx, WS_ISL, isl, &p))) return rc;
+    if ((rc = ws_get(ctx, WS_VAGG, agg, &p))) return rc;
+    if ((rc = ws_get(ctx, WS_IFLG, per_chunk, &p))) return rc;
+    if ((rc = ws_get(ctx, WS_IDONE, per_chunk, &p))) return rc;
     if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nt, CPG_TRAIN_CHUNK), &p))) return rc;
     return CPG_OK;
 }
@@ -260,7 +273,8 @@ int cpg_sync(cpg_ctx* ctx, void* stream) {
 // ---- device entry points ----------------------------------------------------------
 int cpg_count_labelled_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign,
                          int64_t nbases, int64_t chunk_len, int64_t* d_counts, void* stream) {
-    if (!ctx || !d_counts) return set_error(CPG_E_INVALID, "null argument");
+    if (!ctx || !d_counts || (!d_sign && nbases > 0))
+        return set_error(CPG_E_INVALID, "null argument");
     int rc = check_layout(d_packed, nbases, chunk_len);
     if (rc) return rc;
     if (chunk_len % 256) return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 256");
@@ -441,7 +455,7 @@ int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packe
 int cpg_train_pass_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                      const uint32_t* d_sign, int64_t nbases, int64_t chunk_len,
                      double* d_estep_counts, int64_t* d_label_counts, void* stream) {
-    if (!ctx || !model || !d_estep_counts || !d_label_counts)
+    if (!ctx || !model || !d_estep_counts || !d_label_counts || (!d_sign && nbases > 0))
         return set_error(CPG_E_INVALID, "null argument");
     int rc = check_layout(d_packed, nbases, chunk_len);
     if (rc) return rc;

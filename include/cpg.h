@@ -105,13 +105,19 @@ int         cpg_open(int device, cpg_ctx** out);
 void        cpg_close(cpg_ctx* ctx);
 const char* cpg_last_error(void);
 int         cpg_abi_version(void);
-/* Pre-size the context's workspace for inputs of up to nbases bases so that the
- * _d entry points never allocate (required before hipGraph capture). */
+/* Pre-size the context's workspace for inputs of up to nbases bases, for every chunk length
+ * the entry points take (multiples of 4096 up to 1 Mi), so that the _d entry points never
+ * allocate (required before hipGraph capture).  A slot that has to grow later (a larger
+ * input) synchronises the whole device first: the old buffer may still be read by a kernel
+ * on another stream. */
 int         cpg_reserve(cpg_ctx* ctx, int64_t nbases);
 /* Wait for `stream` and return the first kernel-reported status since the last
- * cpg_sync (CPG_OK, CPG_E_VERIFY, CPG_E_INVALID for a broken contig layout, or
- * CPG_E_DEVICE when the island kernel's bounded look-back gave up: the island records
- * and count of that call are then unusable). */
+ * cpg_sync: CPG_OK; CPG_E_VERIFY (a Viterbi exactness self-check failed); CPG_E_INVALID
+ * (a broken contig layout); CPG_E_DEVICE when a bounded look-back gave up — the island
+ * kernel's (the island records and count of that call are unusable) or the Viterbi
+ * segment look-back's (the decoded path and scores of that call are unusable).  The
+ * outputs of cpg_viterbi_d / cpg_decode_d / cpg_islands_d are valid only once cpg_sync
+ * has returned CPG_OK for them. */
 int         cpg_sync(cpg_ctx* ctx, void* stream);
 /* A HIP stream whose kernels run only on the compute units set in cu_mask (mask_words
  * 32-bit words, bit i = compute unit i in the runtime's order): partitions the GPU between
@@ -202,7 +208,9 @@ int cpg_merge_train_d(cpg_ctx* ctx, const void* d_gathered, int world, double* d
 /* Viterbi decode, HmmEvaluator.decode(trainedModel, chunk, true) (:260), of every
  * whole chunk_len chunk (tail not decoded, :256).  Output: the state path as sign bits
  * (state = base + (sign ? 0 : 4)), identical to Mahout's sequential fp64 Viterbi, and
- * the final best log-probability per chunk (d_score, may be NULL).
+ * the final best log-probability per chunk (d_score, may be NULL).  Asynchronous: the
+ * outputs are valid once cpg_sync has returned CPG_OK (the kernels' self-checks and the
+ * segment look-back report through it).
  * Contract: emission rows deterministic (b[i][i%4] == 1), every a[i][j] > 0.  Else
  * CPG_E_UNSUPPORTED.  chunk_len: a multiple of 4096. */
 int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
@@ -228,7 +236,7 @@ int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_s
  * d_score, d_out, *d_count).  When chunk_len is a multiple of 65,536 (the reference's
  * 1 Mi decode chunk) the traceback kernel also writes the island scan's run records from
  * the sign words it produces, so the sign bits are not read back.  Contracts: as the two
- * calls. */
+ * calls; the outputs are valid once cpg_sync has returned CPG_OK. */
 int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                  int64_t nbases, int64_t chunk_len, int64_t first_chunk, uint32_t* d_sign_out,
                  double* d_score, cpg_island* d_out, int64_t cap, int64_t* d_count,
