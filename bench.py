@@ -18,6 +18,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 # kernel arguments in device memory (must precede HIP initialisation)
 os.environ.setdefault("HIP_FORCE_DEV_KERNARG", "1")
 import torch  # noqa: E402
@@ -173,12 +175,256 @@ def _cpu_model():
     return None
 
 
+C3_BASES = 3_100_000_000       # configs[2]: 3.1 Gbp hg38-sized genome over the node's GPUs
+C3_SEED = 20251015 + 2         # seed + config index
+
+
+def _p2p(ops_spec, backend):
+    """Point-to-point transfers [(kind, tensor, peer)] on the current stream (RCCL over xGMI),
+    or staged through host memory for the gloo rehearsal."""
+    D_ = torch.distributed
+    if backend == "nccl":
+        ops = [D_.P2POp(D_.isend if k == "send" else D_.irecv, t, peer) for k, t, peer in ops_spec]
+        for w in D_.batch_isend_irecv(ops):
+            w.wait()
+        return
+    host = []
+    for k, t, peer in ops_spec:
+        h = t.cpu() if k == "send" else torch.empty(t.shape, dtype=t.dtype)
+        host.append((k, t, h, peer))
+    ops = [D_.P2POp(D_.isend if k == "send" else D_.irecv, h, peer) for k, _, h, peer in host]
+    for w in D_.batch_isend_irecv(ops):
+        w.wait()
+    for k, t, h, _ in host:
+        if k == "recv":
+            t.copy_(h)
+
+
+def _gather0(t, world, rank, backend, out_list):
+    """t from every rank to rank 0 (out_list on rank 0), on the current stream."""
+    D_ = torch.distributed
+    if backend == "nccl":
+        D_.gather(t, out_list if rank == 0 else None, dst=0)
+        return
+    h = t.cpu()
+    hl = [torch.empty_like(h) for _ in range(world)] if rank == 0 else None
+    D_.gather(h, hl, dst=0)
+    if rank == 0:
+        for o, x in zip(out_list, hl):
+            o.copy_(x)
+
+
+def run_c3(args, world, rank, local, dist, backend, dev):
+    """configs[2] — the north_star workload: ONE 3.1 Gbp genome split evenly over the world's
+    ranks at multiples of 64 bases (cpgisland_amd/dist.py shard_bounds(align=64), not at chunk
+    boundaries).  A chunk belongs to the rank holding its first base; a rank's last chunk is
+    completed by the halo — the next rank's first bases, received point to point over xGMI
+    (rank r sends its head to r-1) — so every chunk runs whole, through the same kernels as
+    the unsharded run (bit-identical counts, paths and islands: tests/test_dist.py,
+    tests/test_gpu_halo.py).  One step = halo exchange + training pass (E-step + labelled
+    counts) of the rank's training chunks + the reducer (all-gather of the rank records +
+    rank-order merge) + exact Viterbi + islands of its decode chunks + the island records
+    gathered to rank 0.  Strong scaling: value = genome bases per step / step time (max over
+    ranks)."""
+    from cpgisland_amd import Context, HmmModel, baumwelch
+    from cpgisland_amd import device as D
+    from cpgisland_amd import dist as cdist
+    G = args.bases if args.bases != N_PER_GPU else C3_BASES
+    spans = [cdist.shard_bounds(G, world, r, align=cdist.HALO_ALIGN) for r in range(world)]
+    plans = [cdist.shard_plan(s, n, G) for s, n in spans]
+    start, n = spans[rank]
+    pl = plans[rank]
+    for r in range(world - 1):   # (ADVICE r02) every halo comes from the next shard alone
+        if plans[r].halo > spans[r + 1][1]:
+            raise ValueError(f"rank {r}'s halo ({plans[r].halo}) exceeds rank {r + 1}'s shard")
+    log(f"[rank {rank}] C3: genome {G} bases, shard [{start}, {start + n}), local "
+        f"[{pl.base}, {pl.end}) halo {pl.halo}")
+    packed, sign = D.synth_host(C3_SEED, start, n)
+    span = pl.end - pl.base
+    own = min(start + n, pl.end) - pl.base
+    o16, o32 = (pl.base - start) // 16, (pl.base - start) // 32
+    w16, w32 = D.words16(span) + 4, D.words32(span) + 4
+    # the local genome twice (step k uses copy k & 1): the halo of step k+2 is received into
+    # a copy that step k's kernels no longer read
+    bufs = []
+    for _ in range(2):
+        bp = torch.zeros(w16, dtype=torch.int32, device=dev)
+        bs = torch.zeros(w32, dtype=torch.int32, device=dev)
+        if own > 0:
+            bp[:D.words16(own)] = torch.from_numpy(packed[o16:o16 + D.words16(own)].view(np.int32)).to(dev)
+            bs[:D.words32(own)] = torch.from_numpy(sign[o32:o32 + D.words32(own)].view(np.int32)).to(dev)
+        bufs.append((bp, bs))
+    # what this rank sends: its first plans[rank-1].halo bases (static data)
+    ph = plans[rank - 1].halo if rank > 0 else 0
+    head = (torch.from_numpy(packed[:D.words16(ph)].view(np.int32).copy()).to(dev),
+            torch.from_numpy(sign[:D.words32(ph)].view(np.int32).copy()).to(dev)) if ph else None
+    t16, t32 = (start + n - pl.base) // 16, (start + n - pl.base) // 32
+    h16, h32 = D.words16(pl.halo), D.words32(pl.halo)
+    del packed, sign
+    tr_o, tr_n = pl.t0 * TRAIN - pl.base, (pl.t1 - pl.t0) * TRAIN
+    de_o, de_n = pl.d0 * DECODE - pl.base, (pl.d1 - pl.d0) * DECODE
+    ctx = Context(local)
+    ctx.reserve(max(span, 1))
+    model0 = HmmModel.initial()
+    icap = max(4096, de_n // 16384 + 4096)   # island records per rank per step (planted: ~1 per 100 kbp)
+    nd_total = G // DECODE
+    rec = [cdist.train_record(dev) for _ in range(2)]
+    gath = [torch.empty(world * cdist.TRAIN_RECORD, dtype=torch.float64, device=dev) for _ in range(2)]
+    emerged = torch.empty(105, dtype=torch.float64, device=dev)
+    lmerged = torch.empty(124, dtype=torch.int64, device=dev)
+    so = torch.empty(D.words32(max(de_n, 1)) + 4, dtype=torch.int32, device=dev)
+    score = torch.empty(max(pl.d1 - pl.d0, 1), dtype=torch.float64, device=dev)
+    iout = [torch.empty((icap, 32), dtype=torch.uint8, device=dev) for _ in range(2)]
+    icnt = [torch.zeros(1, dtype=torch.int64, device=dev) for _ in range(2)]
+    gat_i = [[torch.empty((icap, 32), dtype=torch.uint8, device=dev) for _ in range(world)]
+             if rank == 0 else None for _ in range(2)]
+    gat_c = [[torch.empty(1, dtype=torch.int64, device=dev) for _ in range(world)]
+             if rank == 0 else None for _ in range(2)]
+    main_s = torch.cuda.current_stream()
+    s_halo, s_tr, s_dec, s_red, s_isl = (torch.cuda.Stream(), torch.cuda.Stream(),
+                                         torch.cuda.Stream(priority=-1), torch.cuda.Stream(),
+                                         torch.cuda.Stream())
+    ev = {k: [torch.cuda.Event() for _ in range(2)] for k in
+          ("halo", "tr_done", "dec_done", "rec", "red", "isl")}
+    ntr = []   # (start, end) timing events of the training pass, every 4th timed step
+
+    # the decode model: one Baum-Welch iteration over the whole genome from the reference's
+    # model (every rank's E-step merged in rank order), before timing
+    def halo_into(b):
+        if world == 1:
+            return
+        ops = []
+        if head is not None:
+            ops += [("send", head[0], rank - 1), ("send", head[1], rank - 1)]
+        if pl.halo:
+            ops += [("recv", bufs[b][0][t16:t16 + h16], rank + 1),
+                    ("recv", bufs[b][1][t32:t32 + h32], rank + 1)]
+        if ops:
+            _p2p(ops, backend)
+    if dist:
+        torch.distributed.barrier()   # (a full collective first: not every rank has a P2P op)
+    for b in range(2):
+        halo_into(b)
+    torch.cuda.synchronize()
+    e0 = D.bw_estep(ctx, model0, bufs[0][0][tr_o // 16:], tr_n, TRAIN)
+    if dist and backend == "nccl":
+        cdist.merge_counts_f64(e0)
+    elif dist:
+        e0.copy_(cdist.merge_counts_f64(e0.cpu()).to(dev))
+    model1 = baumwelch.normalize(e0.cpu().numpy())
+
+    def step(k, timed):
+        b = k & 1
+        bp, bs = bufs[b]
+        with torch.cuda.stream(s_halo):
+            if k >= 2:   # step k-2's kernels have finished reading this copy
+                s_halo.wait_event(ev["tr_done"][b])
+                s_halo.wait_event(ev["dec_done"][b])
+            halo_into(b)
+            ev["halo"][b].record(s_halo)
+        with torch.cuda.stream(s_dec):
+            s_dec.wait_event(ev["halo"][b])
+            if k >= 2:
+                s_dec.wait_event(ev["isl"][b])   # step k-2's island gather has read the records
+            D.decode(ctx, model1, bp[de_o // 16:], de_n, DECODE, cap=icap, first_chunk=pl.d0,
+                     sign_out=so, score=score, out=iout[b], count=icnt[b])
+            ev["dec_done"][b].record(s_dec)
+        with torch.cuda.stream(s_tr):
+            s_tr.wait_event(ev["halo"][b])
+            if k >= 2:
+                s_tr.wait_event(ev["red"][b])    # step k-2's all-gather has read the record
+            mark = timed and k % 4 == 0
+            if mark:
+                ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ea.record(s_tr)
+            D.train_pass(ctx, model0, bp[tr_o // 16:], bs[tr_o // 32:], tr_n, TRAIN,
+                         estep_out=rec[b][1], counts_out=rec[b][2])
+            if mark:
+                eb.record(s_tr)
+                ntr.append((ea, eb))
+            ev["tr_done"][b].record(s_tr)
+        with torch.cuda.stream(s_red):
+            s_red.wait_event(ev["tr_done"][b])
+            cdist.merge_train_records(ctx, rec[b][0], emerged, lmerged, gathered=gath[b])
+            ev["red"][b].record(s_red)
+        with torch.cuda.stream(s_isl):
+            s_isl.wait_event(ev["dec_done"][b])
+            if world > 1:
+                _gather0(icnt[b], world, rank, backend, gat_c[b])
+                _gather0(iout[b], world, rank, backend, gat_i[b])
+            ev["isl"][b].record(s_isl)
+
+    for w in range(args.warmup):
+        step(w, False)
+    torch.cuda.synchronize()
+    ctx.sync(None)
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for it in range(args.steps):
+        step(args.warmup + it, True)
+    issue = time.perf_counter() - t0
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    ctx.sync(None)      # raises if a kernel self-check (exactness) or look-back failed
+    tr_ms = sum(a.elapsed_time(b) for a, b in ntr) / max(1, len(ntr))
+    if dist:
+        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
+        elapsed = float(t.item())
+    last = (args.warmup + args.steps - 1) & 1
+    counts = [int(c.item()) for c in gat_c[last]] if (rank == 0 and world > 1) else \
+        [int(icnt[last].item())]
+    if max(counts) > icap:
+        raise RuntimeError(f"island records per rank {max(counts)} exceed the gather capacity {icap}")
+    if rank == 0:
+        ms = elapsed * 1e3 / args.steps
+        value = G * args.steps / elapsed
+        bpb = BYTES_PER_BASE["estep"] + 0.125
+        ach = bpb * tr_n / (tr_ms / 1e3) / 1e9 if tr_ms > 0 else 0.0
+        out = {"metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
+               "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+               "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
+               "dtype": "f64", "data": f"synthetic (counter-based planted-island genome, seed {C3_SEED})",
+               "config": {"workload": f"C3: {G / 1e9:.1f} Gbp hg38-sized genome split over "
+                                      f"{world} GPU(s) at 64-base boundaries; halo P2P + BW "
+                                      "E-step + labelled counts + RCCL reduce + exact Viterbi + "
+                                      "islands + island gather to rank 0",
+                          "genome_bases": G, "bases_per_gpu": n, "parallelism": f"dp{world}",
+                          "train_chunk": TRAIN, "decode_chunk": DECODE,
+                          "decode_chunks": nd_total, "island_capacity_per_rank": icap,
+                          "collectives": (("rccl" if backend == "nccl" else backend)
+                                          if dist else None),
+                          "islands_found": sum(counts)},
+               "phases_ms": {"train_pass": round(tr_ms, 4)},
+               "host_issue_ms_per_step": round(issue * 1e3 / args.steps, 4),
+               "roofline": {"bound": "hbm", "kernel": "k_estep_chunk<true>", "phase": "train_pass",
+                            "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                            "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
+                            "algorithmic_bytes": bpb * tr_n, "bytes_per_base": bpb},
+               "cpu_baseline": None}
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if dist:
+        torch.distributed.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=20)
-    ap.add_argument("--bases", type=int, default=N_PER_GPU, help="bases per GPU")
+    ap.add_argument("--bases", type=int, default=N_PER_GPU,
+                    help="bases per GPU (C2), or the whole genome with --workload c3 "
+                         "(default there: 3.1e9)")
+    ap.add_argument("--workload", choices=("auto", "c2", "c3"), default="auto",
+                    help="c2: 46 Mbp per GPU (configs[1], weak scaling); c3: one 3.1 Gbp genome "
+                         "split over the GPUs (configs[2], the north_star workload, strong "
+                         "scaling); auto: c2 on one GPU, c3 on several")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--probe-sleep", type=str, default="",
                     help="measurement probe: STREAM:CYCLES adds a one-thread spin kernel "
@@ -266,6 +512,9 @@ def main():
             torch.distributed.init_process_group(backend)
     dev = torch.device("cuda", local)
     torch.cuda.set_device(dev)
+    workload = args.workload if args.workload != "auto" else ("c3" if dist else "c2")
+    if workload == "c3":
+        return run_c3(args, world, rank, local, dist, backend, dev)
 
     from cpgisland_amd import Context, HmmModel
     from cpgisland_amd import device as D

@@ -227,3 +227,58 @@ def test_shard_plans_cover_every_chunk_once(n, world):
         assert p.halo < _lib.DECODE_CHUNK
     with pytest.raises(ValueError):
         cd.shard_plan(100, 64, n)                   # not a multiple of 64
+
+
+# ---------------------------------------------------------------- bench.py's C3 step transfers
+def _c3_comm_worker(rank, world, port, q):
+    """bench.py's C3 halo (point to point: rank r sends its first plans[r-1].halo bases to
+    r-1, received into the tail of r-1's local buffer) and island gather to rank 0, with the
+    gloo staging of the rehearsal path, on CPU tensors."""
+    import importlib.util
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        spec = importlib.util.spec_from_file_location(
+            "bench", os.path.join(os.path.dirname(os.path.dirname(__file__)), "bench.py"))
+        bench = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(bench)
+        obs, truth = _genome()
+        spans = [cd.shard_bounds(N, world, r, align=cd.HALO_ALIGN) for r in range(world)]
+        plans = [cd.shard_plan(s, n, N, train=TRAIN, decode=DECODE) for s, n in spans]
+        start, n = spans[rank]
+        pl = plans[rank]
+        own = pr.pack(obs[start:start + n]).view(np.int32)
+        span = pl.end - pl.base
+        buf = torch.zeros((span + 15) // 16 + 4, dtype=torch.int32)
+        ow = min(start + n, pl.end) - pl.base
+        o16 = (pl.base - start) // 16
+        buf[:(ow + 15) // 16] = torch.from_numpy(own[o16:o16 + (ow + 15) // 16].copy())
+        ops = []
+        ph = plans[rank - 1].halo if rank > 0 else 0
+        if ph:
+            ops.append(("send", torch.from_numpy(own[:(ph + 15) // 16].copy()), rank - 1))
+        if pl.halo:
+            t16 = (start + n - pl.base) // 16
+            ops.append(("recv", buf[t16:t16 + (pl.halo + 15) // 16], rank + 1))
+        if ops:
+            bench._p2p(ops, "gloo")
+        got = pr.unpack(buf.numpy().view(np.uint32), span)
+        ok_halo = bool(np.array_equal(got, obs[pl.base:pl.end]))
+        recs = torch.full((3, 4), rank, dtype=torch.int64)
+        outs = [torch.empty(3, 4, dtype=torch.int64) for _ in range(world)] if rank == 0 else None
+        bench._gather0(recs, world, rank, "gloo", outs)
+        ok_gather = rank != 0 or all(bool((o == r).all()) for r, o in enumerate(outs))
+        q.put((rank, pl.halo, ok_halo, ok_gather))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_bench_c3_halo_p2p_and_island_gather(world):
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    mp.start_processes(_c3_comm_worker, args=(world, _free_port(), q), nprocs=world, join=True,
+                       start_method="spawn")
+    res = sorted([q.get() for _ in range(world)])
+    assert any(r[1] > 0 for r in res)             # some rank's last chunk needed the halo
+    assert all(r[2] for r in res) and all(r[3] for r in res)

@@ -21,6 +21,18 @@ if [[ $STEPS == *bench* ]]; then
   rc=$?; echo "bench(400) rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/bench_400.err; exit $rc; }
   python3 -c "import json; d=json.load(open('$OUT/bench_400.json')); print('400', round(d['value']/1e9,1), d['ms_per_step'], d['phases_ms'])"
 fi
+if [[ $STEPS == *c3* ]]; then
+  # the north_star workload: the whole 3.1 Gbp genome on this GPU, then the 2-rank path
+  # rehearsed on the one GPU (gloo collectives staged through host memory)
+  timeout -k 10 600 python bench.py --workload c3 --steps 10 --warmup 3 > $OUT/c3_n1.json 2> $OUT/c3_n1.err
+  rc=$?; echo "c3 n1 rc=$rc"; [ $rc -eq 0 ] || { tail -20 $OUT/c3_n1.err; exit $rc; }
+  python3 -c "import json; d=json.load(open('$OUT/c3_n1.json')); print('c3 n1', round(d['value']/1e9,1), d['ms_per_step'], d['phases_ms'], d['config']['islands_found'])"
+  CPG_BENCH_BACKEND=gloo timeout -k 10 900 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 \
+      --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 \
+      > $OUT/c3_gloo2.json 2> $OUT/c3_gloo2.err
+  rc=$?; echo "c3 gloo2 rc=$rc"; [ $rc -eq 0 ] || { tail -30 $OUT/c3_gloo2.err; exit $rc; }
+  python3 -c "import json; d=json.load(open('$OUT/c3_gloo2.json')); print('c3 gloo2', round(d['value']/1e9,1), d['ms_per_step'], d['config']['islands_found'])"
+fi
 if [[ $STEPS == *prof* ]]; then
   R=$(pwd); cd /tmp && export TMPDIR=/tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d $R/$OUT/prof -o run --output-format csv \
