@@ -71,6 +71,7 @@ SIGNATURES = {
     "cpg_train_pass_d": [_P, _P, _P, _P, _I64, _I64, _P, _P, _P],
     "cpg_merge_train_d": [_P, _P, _INT, _P, _P, _P],
     "cpg_viterbi_d": [_P, _P, _P, _I64, _I64, _P, _P, _P],
+    "cpg_viterbi_states_d": [_P, _P, _P, _I64, _I64, _P, _P, _P],
     "cpg_islands_d": [_P, _P, _P, _I64, _I64, _P, _I64, _P, _P],
     "cpg_islands_at_d": [_P, _P, _P, _I64, _I64, _I64, _P, _I64, _P, _P],
     "cpg_decode_d": [_P, _P, _P, _I64, _I64, _I64, _P, _P, _P, _I64, _P, _P],

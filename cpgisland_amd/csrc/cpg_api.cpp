@@ -135,6 +135,22 @@ int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out) {
 
 namespace {
 
+// the general-model Viterbi (k_vit_general.hip) over nch whole chunks of C bases
+int vit_general(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed, int64_t nch,
+                int64_t C, uint8_t* d_states, double* d_score, uint32_t* d_sign, uint32_t** spk,
+                bool check_sign, hipStream_t s) {
+    if (nch > 1 && C % 16)
+        return set_error(CPG_E_INVALID, "chunk_len must be a multiple of 16 for >1 chunk");
+    GenConsts gc;
+    gen_prepare(model, &gc);
+    void* ws;
+    int rc;
+    if ((rc = ws_get(ctx, WS_VGEN, vitg_ws_bytes(nch, C), &ws))) return rc;
+    CPG_HIP(launch_vitg(gc, d_packed, nch, C, ws, ctx->ws[WS_VGEN].bytes, d_states, d_score,
+                        d_sign, spk, ctx->d_status, check_sign, s));
+    return CPG_OK;
+}
+
 int check_layout(const void* packed, int64_t nbases, int64_t chunk_len) {
     if (!packed && nbases > 0) return set_error(CPG_E_INVALID, "null packed buffer");
     if (nbases < 0 || chunk_len <= 0)
@@ -252,6 +268,11 @@ int cpg_sync(cpg_ctx* ctx, void* stream) {
             return set_error(CPG_E_DEVICE,
                              "viterbi: the look-back over a chunk's earlier segments timed out; "
                              "the decoded path is unusable (status 0x%x)", st);
+        if (st & ST_GEN_NOT_SIGN)
+            return set_error(CPG_E_UNSUPPORTED,
+                             "viterbi (general model): the decoded path visits states that are "
+                             "not their position's base (a dead end of zero transitions); sign "
+                             "bits cannot carry it: use cpg_viterbi_states_d (status 0x%x)", st);
         if (st & ST_LOOKBACK_TIMEOUT)
             return set_error(CPG_E_DEVICE,
                              "island records: the look-back over earlier chunks' counts timed "
@@ -307,6 +328,19 @@ int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed
     const int64_t w_done = (nch * chunk_len + 31) / 32, w_all = (nbases + 31) / 32;
     const int64_t ntail = w_all > w_done ? w_all - w_done : 0;
     if (nch == 0) {
+        if (ntail) CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)ntail * 4, s));
+        return CPG_OK;
+    }
+    if (!vit_fast_ok(model)) {
+        // outside the exact scan's contract: Mahout's 8-state loop itself (k_vit_general.hip)
+        if (model_check_deterministic(model))
+            return set_error(CPG_E_UNSUPPORTED,
+                             "emission matrix not deterministic: the path's states are not "
+                             "base + (sign ? 0 : 4), so sign bits cannot carry it; use "
+                             "cpg_viterbi_states_d or cpg_decode_d");
+        if ((rc = vit_general(ctx, model, d_packed, nch, chunk_len, nullptr, d_score, d_sign_out,
+                              nullptr, true, s)))
+            return rc;
         if (ntail) CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)ntail * 4, s));
         return CPG_OK;
     }
@@ -396,6 +430,20 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
         CPG_HIP(hipMemsetAsync(d_count, 0, sizeof(int64_t), s));
         return CPG_OK;
     }
+    if (!vit_fast_ok(model)) {
+        // any model (k_vit_general.hip): the states as sign bits (state < 4) and state-packed
+        // words (state & 3), over which the island kernels run the :262-339 loop on the
+        // states themselves
+        uint32_t* spk = nullptr;
+        if ((rc = vit_general(ctx, model, d_packed, nch, chunk_len, nullptr, d_score, d_sign_out,
+                              &spk, false, s)))
+            return rc;
+        if (ntail) CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)ntail * 4, s));
+        CPG_HIP(launch_islands(spk, d_sign_out, nch, chunk_len, first_chunk, wsi,
+                               ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status, s,
+                               static_cast<unsigned long long*>(fl)));
+        return CPG_OK;
+    }
     VitConsts vc;
     static thread_local VitTables vt;
     if ((rc = vit_prepare(model, chunk_len, &vc, &vt))) return rc;
@@ -429,6 +477,21 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                            ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status, s,
                            static_cast<unsigned long long*>(fl)));
     return CPG_OK;
+}
+
+int cpg_viterbi_states_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                         int64_t nbases, int64_t chunk_len, uint8_t* d_states_out,
+                         double* d_score, void* stream) {
+    if (!ctx || !model || (!d_states_out && nbases >= chunk_len))
+        return set_error(CPG_E_INVALID, "null argument");
+    int rc = check_layout(d_packed, nbases, chunk_len);
+    if (rc) return rc;
+    const int64_t nch = nbases / chunk_len;
+    if (nch == 0) return CPG_OK;
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    return vit_general(ctx, model, d_packed, nch, chunk_len, d_states_out, d_score, nullptr,
+                       nullptr, false, pick(ctx, stream));
 }
 
 int cpg_bw_estep_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
@@ -596,6 +659,22 @@ int cpg_decode_states(cpg_ctx* ctx, const cpg_model* model, const int32_t* obs, 
                              "observation %lld = %d not in 0..3 (reference: "
                              "ArrayIndexOutOfBoundsException)", (long long)i, obs[i]);
         packed[i >> 4] |= (uint32_t)obs[i] << ((i & 15) * 2);
+    }
+    if (!vit_fast_ok(model)) {   // any model: Mahout's 8-state loop (k_vit_general.hip)
+        void *dp, *dst;
+        {
+            std::lock_guard<std::mutex> lk(ctx->mu);
+            CPG_HIP(hipSetDevice(ctx->device));
+            CPG_TRY(stage_in(ctx, WS_IN0, packed.data(), packed.size() * 4, &dp));
+            CPG_TRY(ws_get(ctx, WS_OUT0, (size_t)n + 64, &dst));
+            CPG_TRY(vit_general(ctx, model, (const uint32_t*)dp, 1, n, (uint8_t*)dst, nullptr,
+                                nullptr, nullptr, false, ctx->stream));
+        }
+        std::vector<uint8_t> st((size_t)n);
+        CPG_HIP(hipMemcpyAsync(st.data(), dst, (size_t)n, hipMemcpyDeviceToHost, ctx->stream));
+        CPG_TRY(cpg_sync(ctx, ctx->stream));
+        for (int64_t i = 0; i < n; ++i) states_out[i] = st[i];
+        return CPG_OK;
     }
     std::vector<uint32_t> sign((size_t)(n + 31) / 32 + 4, 0u);
     double score = 0.0;

@@ -38,6 +38,28 @@ int model_check_deterministic(const cpg_model* m) {
     return CPG_OK;
 }
 
+bool vit_fast_ok(const cpg_model* m) {
+    for (int i = 0; i < 8; ++i) {
+        for (int k = 0; k < 4; ++k)
+            if (m->b[i][k] != ((k == i % 4) ? 1.0 : 0.0)) return false;
+        if (!(m->pi[i] >= 0.0 && m->pi[i] <= 1.0)) return false;
+        for (int j = 0; j < 8; ++j)
+            if (!(m->a[i][j] > 0.0 && m->a[i][j] <= 1.0)) return false;
+    }
+    return true;
+}
+
+// the general path's constants: every log Mahout's loop takes, C library log
+void gen_prepare(const cpg_model* m, GenConsts* gc) {
+    for (int j = 0; j < 8; ++j)
+        for (int i = 0; i < 8; ++i) gc->L[j][i] = std::log(m->a[j][i]);
+    for (int i = 0; i < 8; ++i)
+        for (int k = 0; k < 4; ++k) {
+            gc->LB[i][k] = std::log(m->b[i][k]);
+            gc->LP[i][k] = std::log(m->pi[i] * m->b[i][k]);
+        }
+}
+
 // Viterbi constants.  L = log a exactly as Mahout evaluates Math.log(a.getQuick(j, i))
 // (here: the C library log, shared by every kernel and by the oracle).
 int vit_prepare(const cpg_model* m, int64_t chunk_len, VitConsts* vc, VitTables* vt) {

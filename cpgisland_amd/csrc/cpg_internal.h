@@ -33,6 +33,8 @@ enum : uint32_t {
     ST_CONTIG_LAYOUT = 1u << 3,  // a contig breaks the batch layout contract (skipped)
     ST_LOOKBACK_TIMEOUT = 1u << 4,   // a bounded look-back spin gave up (records unusable)
     ST_VIT_LOOKBACK = 1u << 5,       // the Viterbi segment look-back gave up (path unusable)
+    ST_GEN_NOT_SIGN = 1u << 6,       // general-model path: a state is not its base's (the path
+                                     // is not representable as sign bits)
 };
 
 // ---- Viterbi constants (host-computed, shared by every kernel) ---------------------
@@ -48,6 +50,13 @@ struct VitConsts {
     double spread;          // 2*|min L|: lower slack inside a block
     int emin, emax;         // binades with exact tables
     uint64_t tie_mask;      // binade e has a rounding tie -> never regular
+};
+// the general-model Viterbi's constants (k_vit_general.hip): Math.log of every model entry
+// Mahout's loop takes the log of, computed on the host (C library log, as the oracle's)
+struct GenConsts {
+    double L[8][8];     // log a[j][i]
+    double LB[8][4];    // log b[i][k]
+    double LP[8][4];    // log(pi[i] * b[i][k])
 };
 // per-binade rounded constants Le[e][16][4], e in [0, kMaxBinade)
 struct VitTables {
@@ -123,7 +132,9 @@ enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5,
        WS_VAGG = 16, WS_IFLG = 17,
        // per-chunk done counters of the fused decode: zero between calls (zero-filled when
        // allocated, reset by the workgroup that completes a chunk), so a slot of their own
-       WS_IDONE = 18, WS_NSLOT = 19 };
+       WS_IDONE = 18,
+       // the general-model Viterbi (backpointer ballots, states, state-packed words)
+       WS_VGEN = 19, WS_NSLOT = 20 };
 // a fresh look-back tag per call: an odd multiple of a counter (a bijection: distinct for 2^32
 // calls), never 0 (zero-filled workspace) or all ones
 uint32_t lookback_epoch();
@@ -168,6 +179,10 @@ int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitConsts& vc, const VitT
                const VitTables** out);
 int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out);
 int vit_prepare(const cpg_model* m, int64_t chunk_len, VitConsts* vc, VitTables* vt);
+// the exact parallel Viterbi's model contract (deterministic emissions, 0 < a <= 1,
+// 0 <= pi <= 1); models outside it decode through the general path
+bool vit_fast_ok(const cpg_model* m);
+void gen_prepare(const cpg_model* m, GenConsts* gc);
 
 // kernel launchers (defined in the .hip files); all asynchronous on `s`
 // parts: bit 0 = accumulate the chunks into the context's fixed-point accumulators, bit 1 =
@@ -186,6 +201,15 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                           const IslFuse* fuse = nullptr,    // fused decode: K7 resolves
                           unsigned int* done5 = nullptr);   // nchunks zeroed words: K5 runs K6
 size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len);
+// the general-model Viterbi (any model: k_vit_general.hip): states_out (nchunks * C bytes, or
+// the workspace when null), score (may be null), sign_out (state < 4; may be null), *spk_out
+// (state & 3 in the packed layout, in the workspace; may be null); check_sign: status bit
+// ST_GEN_NOT_SIGN when a state is not its position's base (state & 3 != base)
+size_t vitg_ws_bytes(int64_t nchunks, int64_t C);
+hipError_t launch_vitg(const GenConsts& gc, const uint32_t* packed, int64_t nchunks, int64_t C,
+                       void* ws, size_t ws_bytes, uint8_t* states_out, double* score,
+                       uint32_t* sign_out, uint32_t** spk_out, uint32_t* status,
+                       bool check_sign, hipStream_t s);
 size_t viterbi_agg_bytes(int64_t nchunks, int64_t chunk_len);   // WS_VAGG
 // model-derived LDS tables of K1/K3, built once per model right after the VitTables copy
 size_t vit_derived_bytes();

@@ -429,10 +429,11 @@ __global__ __launch_bounds__(kCT, kCtgEstWaves) void k_ctg_estep(Ctg a, cpg_mode
                         const int p = 16 * k + j;
                         if (p >= left) continue;
                         if (i == 0 && p == 0) {   // gamma_0 -> init counts
+                            // (2^-54 units: <= kCT contigs per round stay below 2^62)
                             const double gp = alP[0] * yP, gm = alM[0] * yM, z = gp + gm;
-                            const double r = rcp_nr(z) * kFixC;
-                            atomicAdd(&sinit[o0], to_fixed_scaled(gp * r));
-                            atomicAdd(&sinit[o0 + 4], to_fixed_scaled(gm * r));
+                            const double r = rcp_nr(z) * 18014398509481984.0;   // 2^54
+                            atomicAdd(&sinit[o0], __double2ull_rn(gp * r));
+                            atomicAdd(&sinit[o0 + 4], __double2ull_rn(gm * r));
                             continue;
                         }
                         const double uP = j > 0 ? alP[j - 1] : eP;
@@ -457,15 +458,15 @@ __global__ __launch_bounds__(kCT, kCtgEstWaves) void k_ctg_estep(Ctg a, cpg_mode
             }
         }
         __syncthreads();
-        // flush: bins (2^-38) -> the 128-bit accumulators (2^-47): shift by 9
+        // flush: bins (2^-38) -> the 128-bit accumulators (2^-47; init rows 2^-54 -> 2^-62)
         if (t < 64) {   // t = k * 16 + d  ->  slab row d * 4 + k
             unsigned long long s = 0;
 #pragma unroll
             for (int col = 0; col < 16; ++col) s += bins[t * 16 + ((col + t) & 15)];
             if (s) acc128_add2(acc + 2 * ((t & 15) * 4 + (t >> 4)), s << 9, s >> 55);
-        } else if (t < 72) {
+        } else if (t < 72) {   // init rows: 2^-54 -> 2^-62 (k_estep.hip kFixInit): shift by 8
             const unsigned long long s = sinit[t - 64];
-            if (s) acc128_add2(acc + 2 * t, s << 9, s >> 55);
+            if (s) acc128_add2(acc + 2 * t, s << 8, s >> 56);
         } else if (t == 72) {
             const long long L = sll;
             if (L) acc128_add2(acc + 2 * 72, (unsigned long long)L, L < 0 ? ~0ull : 0ull);

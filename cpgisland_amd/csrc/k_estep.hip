@@ -187,6 +187,13 @@ __device__ __forceinline__ unsigned long long class_count(unsigned long long S) 
     return ((q >> 3) * 0xF641ull) & 0x1FFFFull;
 }
 constexpr int kLogFix = 24;   // log-likelihood fixed point: 2^-24 (|chunk loglik| < 2^30)
+// init posteriors (one gamma_0 per chunk and state): fixed point 2^-62, so that a state whose
+// gamma_0 is small keeps full relative precision (on the xi bins' 2^-47 grid a chunk's
+// gamma_0 of 1e-3 carried a relative error of up to 3.6e-12, summed over the chunks)
+constexpr double kFixInit = 4611686018427387904.0;   // 2^62
+__device__ __forceinline__ unsigned long long to_fixed_init(double y47) {   // y47 = gamma_0 * 2^47
+    return __double2ull_rn(ldexp(y47, 15));
+}
 
 // 128-bit two's-complement accumulation with 64-bit atomics: the adder that wraps the low
 // word carries into the high word (plus the sign extension of a negative addend)
@@ -572,8 +579,8 @@ constexpr int kPFD = 1;   // backward table rows loaded this many positions ahea
                     // added at once (nothing stays live across the main loop for it)
                     const uint32_t b0 = pk[0] & 3u;
                     unsigned long long* ra = acc + 2 * kSlab * (c % kAccRep);
-                    acc128_add(ra + 2 * (64 + b0), to_fixed_scaled(alP[0] * yP), false);
-                    acc128_add(ra + 2 * (64 + b0 + 4), to_fixed_scaled(alM[0] * yM), false);
+                    acc128_add(ra + 2 * (64 + b0), to_fixed_init(alP[0] * yP), false);
+                    acc128_add(ra + 2 * (64 + b0 + 4), to_fixed_init(alM[0] * yM), false);
                     continue;
                 }
                 const double uP = i > lo ? alP[i - 1 - lo] : (lo > 0 ? hP : bfP);
@@ -661,7 +668,8 @@ __device__ void finalize(unsigned long long* acc, double* vsum, double* out) {
             hi = ~hi + (lo == 0ull ? 1ull : 0ull);
         }
         const double mag = (double)hi * 18446744073709551616.0 + (double)lo;
-        vsum[i] = i < 72 ? mag * (1.0 / kFix) : ldexp(neg ? -mag : mag, -kLogFix);
+        vsum[i] = i < 64 ? mag * (1.0 / kFix)
+                : i < 72 ? mag * (1.0 / kFixInit) : ldexp(neg ? -mag : mag, -kLogFix);
     }
     __syncthreads();
     for (int i = t; i < 2 * kSlab * kAccRep; i += blockDim.x) acc[i] = 0ull;

@@ -120,6 +120,22 @@ def viterbi(ctx: Context, model: HmmModel, packed: torch.Tensor, nbases: int,
     return sign_out, score
 
 
+def viterbi_states(ctx: Context, model: HmmModel, packed: torch.Tensor, nbases: int,
+                   chunk_len: int = _lib.DECODE_CHUNK, states_out: torch.Tensor | None = None,
+                   score: torch.Tensor | None = None):
+    """HmmEvaluator.decode for ANY model (cpg_viterbi_states_d): one uint8 state per position
+    of the whole chunks, and the best log-probability per chunk.  Returns (states, score)."""
+    nch = nbases // chunk_len
+    if states_out is None:
+        states_out = torch.empty(max(nch * chunk_len, 1), dtype=torch.uint8, device=packed.device)
+    if score is None:
+        score = torch.empty(max(nch, 1), dtype=torch.float64, device=packed.device)
+    m = model.to_struct()
+    check(lib.cpg_viterbi_states_d(ctx.handle, ptr(m), _dp(packed), nbases, chunk_len,
+                                   _dp(states_out), _dp(score), _stream()))
+    return states_out, score
+
+
 def islands(ctx: Context, packed: torch.Tensor, sign: torch.Tensor, nbases: int,
             chunk_len: int = _lib.DECODE_CHUNK, cap: int = 1 << 20, first_chunk: int = 0,
             out: torch.Tensor | None = None, count: torch.Tensor | None = None):

@@ -211,11 +211,28 @@ int cpg_merge_train_d(cpg_ctx* ctx, const void* d_gathered, int world, double* d
  * the final best log-probability per chunk (d_score, may be NULL).  Asynchronous: the
  * outputs are valid once cpg_sync has returned CPG_OK (the kernels' self-checks and the
  * segment look-back report through it).
- * Contract: emission rows deterministic (b[i][i%4] == 1), every a[i][j] > 0.  Else
- * CPG_E_UNSUPPORTED.  chunk_len: a multiple of 4096. */
+ * Models: the exact parallel scan takes deterministic emission rows (b[i][i%4] == 1),
+ * 0 < a[i][j] <= 1 and 0 <= pi[i] <= 1; other models with deterministic emission rows (zero
+ * transitions, pi outside) run Mahout's 8-state loop (cpg_viterbi_states_d's path), and
+ * cpg_sync reports CPG_E_UNSUPPORTED if their path leaves the bases' states (a dead end of
+ * zero transitions: sign bits cannot carry it); non-deterministic emission rows:
+ * CPG_E_UNSUPPORTED at once (use cpg_viterbi_states_d or cpg_decode_d).  chunk_len: a
+ * multiple of 256 when there is more than one chunk. */
 int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                   int64_t nbases, int64_t chunk_len, uint32_t* d_sign_out,
                   double* d_score, void* stream);
+
+/* HmmEvaluator.decode(model, chunk, true) (:260) for ANY model the reference accepts (zero
+ * transition probabilities, emission rows that are not deterministic, pi with zeros):
+ * Mahout's 8-state recurrence itself, bit-identical, chunks in parallel.
+ * d_states_out: one byte per position of the whole chunks (states 0..7; bytes past the last
+ * whole chunk are not written); d_score: best log-probability per chunk (may be NULL).
+ * chunk_len: a multiple of 16 when there is more than one chunk.  A correctness path
+ * (~1 Gbase/s): cpg_viterbi_d / cpg_decode_d take it themselves for models outside the
+ * exact scan's contract. */
+int cpg_viterbi_states_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
+                         int64_t nbases, int64_t chunk_len, uint8_t* d_states_out,
+                         double* d_score, void* stream);
 
 /* Island scan + filter, CpGIslandFinder.java:262-339, over every whole chunk.
  * d_out: capacity `cap` records; *d_count (device int64) receives the number of
@@ -235,8 +252,11 @@ int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_s
  * cpg_islands_at_d(first_chunk) on the same buffers, with identical outputs (d_sign_out,
  * d_score, d_out, *d_count).  When chunk_len is a multiple of 65,536 (the reference's
  * 1 Mi decode chunk) the traceback kernel also writes the island scan's run records from
- * the sign words it produces, so the sign bits are not read back.  Contracts: as the two
- * calls; the outputs are valid once cpg_sync has returned CPG_OK. */
+ * the sign words it produces, so the sign bits are not read back.  Any model: outside the
+ * exact scan's contract the decode runs Mahout's 8-state loop (cpg_viterbi_states_d's path),
+ * d_sign_out then holding state < 4 and the island scan running on the states themselves
+ * (the :262-339 loop reads only them).  The outputs are valid once cpg_sync has returned
+ * CPG_OK. */
 int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                  int64_t nbases, int64_t chunk_len, int64_t first_chunk, uint32_t* d_sign_out,
                  double* d_score, cpg_island* d_out, int64_t cap, int64_t* d_count,
