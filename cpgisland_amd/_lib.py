@@ -98,6 +98,17 @@ def _load():
         raise ImportError(
             f"libcpg.so not built at {LIB_PATH}: run `make -C cpgisland_amd/csrc` "
             "(there is no CPU fallback for the hot path)")
+    # ONE HIP runtime per process: torch bundles its own libamdhip64 (soname libamdhip64.so.7,
+    # the same as /opt/rocm's, which libcpg.so needs), but torch's libraries ask for it as
+    # "libamdhip64.so".  Loaded after libcpg.so, torch therefore maps a second runtime beside
+    # the first, and whichever initialises second finds no device (seen on the GPU box when
+    # this package was imported before torch).  Loaded first, torch's runtime is the one
+    # libcpg.so's dependency resolves to.  (A host without torch — the Java FFM binding — uses
+    # /opt/rocm's runtime alone.)
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     for name, args in SIGNATURES.items():
         fn = getattr(lib, name)

@@ -233,10 +233,19 @@ def test_decode_errors(gpu_ctx):
         HmmEvaluator.decode(m, np.array([0, 1, 4], np.int32), ctx=gpu_ctx)
     with pytest.raises(CpgInvalid):
         HmmEvaluator.decode(m, np.array([], np.int32), ctx=gpu_ctx)
-    bad = HmmModel.initial()
-    bad.b[0] = [0.9, 0.1, 0, 0]
+    # a non-deterministic emission row: HmmEvaluator.decode takes it (the general-model path,
+    # tests/test_gpu_general.py) and matches the oracle; sign bits cannot carry such a path,
+    # so cpg_viterbi_d refuses it
+    nd = HmmModel.initial()
+    nd.b[0] = [0.9, 0.1, 0, 0]
+    obs = np.array([0, 1, 2], np.int32)
+    ref, _ = co.viterbi8(nd.to_struct(), obs.astype(np.uint8))
+    assert np.array_equal(HmmEvaluator.decode(nd, obs, ctx=gpu_ctx), ref)
+    import torch
+    from cpgisland_amd import device as D
+    dp = D.to_device(np.zeros(4096 // 16 + 8, np.uint32), torch.device("cuda:0"))
     with pytest.raises(CpgError) as e:
-        HmmEvaluator.decode(bad, np.array([0, 1, 2], np.int32), ctx=gpu_ctx)
+        D.viterbi(gpu_ctx, nd, dp, 4096, 4096)
     assert e.value.code == _lib.CPG_E_UNSUPPORTED
 
 
