@@ -266,7 +266,7 @@ def run_c3(args, world, rank, local, dist, backend, dev):
     ctx = Context(local)
     ctx.reserve(max(span, 1))
     model0 = HmmModel.initial()
-    icap = max(4096, de_n // 16384 + 4096)   # island records per rank per step (planted: ~1 per 100 kbp)
+    icap = de_n // 32768 + 2048   # island records per rank per step (~3x the ~1 per 100 kbp)
     nd_total = G // DECODE
     rec = [cdist.train_record(dev) for _ in range(2)]
     gath = [torch.empty(world * cdist.TRAIN_RECORD, dtype=torch.float64, device=dev) for _ in range(2)]
