@@ -287,3 +287,34 @@ def test_golden_vectors_reproduce():
         st, _ = co.viterbi8(m, o)
         assert np.array_equal(st, g[f"small{k}_states"])
         assert np.array_equal(co.estep(m, o, len(o)), g[f"small{k}_estep"])
+
+
+def test_dead_end_model_both_restatements():
+    """Zero transitions C+/C- -> G+/G-: after a 'CG' every candidate is -inf, so (A.2) every
+    later delta is -inf, every later backpointer 0 and the final state 0 — both restatements
+    agree on states and score (the steps before the dead end keep their real argmax)."""
+    pi, a, b = co.model_split(m0())
+    a3 = a.copy()
+    a3[np.ix_([1, 5], [2, 6])] = 0.0
+    a3 /= a3.sum(1, keepdims=True)
+    m3 = co.model_flat(pi, a3, b)
+    obs = np.array([0, 3, 1, 2, 0, 1, 3], np.uint8)
+    st, best = co.viterbi8(m3, obs)
+    # from the dead end (t = 3) on, and at t = 2 through its backpointer, the path is state 0
+    assert best == -np.inf and list(st[2:]) == [0] * (len(obs) - 2)
+    seq, mp = pr.viterbi8(m3[:8].tolist(), m3[8:72].reshape(8, 8).tolist(),
+                          m3[72:].reshape(8, 4).tolist(), obs.tolist())
+    assert seq == list(st) and mp == best
+
+
+def test_non_deterministic_emissions_both_restatements():
+    rng = np.random.default_rng(7)
+    b = rng.random((8, 4))
+    b /= b.sum(1, keepdims=True)
+    pi, a, _ = co.model_split(m0())
+    m = co.model_flat(pi, a, b)
+    obs = rng.integers(0, 4, 300).astype(np.uint8)
+    st, best = co.viterbi8(m, obs)
+    seq, mp = pr.viterbi8(m[:8].tolist(), m[8:72].reshape(8, 8).tolist(),
+                          m[72:].reshape(8, 4).tolist(), obs.tolist())
+    assert seq == list(st) and mp == best
