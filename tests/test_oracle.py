@@ -300,8 +300,8 @@ def test_dead_end_model_both_restatements():
     m3 = co.model_flat(pi, a3, b)
     obs = np.array([0, 3, 1, 2, 0, 1, 3], np.uint8)
     st, best = co.viterbi8(m3, obs)
-    # from the dead end (t = 3) on, and at t = 2 through its backpointer, the path is state 0
-    assert best == -np.inf and list(st[2:]) == [0] * (len(obs) - 2)
+    # from the dead end (t = 3) on the path is state 0; before it the real argmax
+    assert best == -np.inf and list(st[3:]) == [0] * (len(obs) - 3) and st[2] == 1
     seq, mp = pr.viterbi8(m3[:8].tolist(), m3[8:72].reshape(8, 8).tolist(),
                           m3[72:].reshape(8, 4).tolist(), obs.tolist())
     assert seq == list(st) and mp == best
