@@ -519,11 +519,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
             for (int i = 0; i < hi; ++i) {
                 if (!(t == 0 && m == 0 && i == 0)) {   // (alpha_0 itself at the chunk start)
                     const uint32_t d = code_at(cm, i);
-#ifdef EST_FWD_GLOBAL   // (temporary A/B)
-                    const double2 ma = gtab[d], mb = gtab[16 + d];
-#else
                     const double2 ma = TA[d], mb = TB[d];
-#endif
                     const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
                     xP = nP;
                     xM = nM;
