@@ -49,7 +49,7 @@ def _ingest(ctx: Context, path: str, mode: int):
     d_txt = D.text_to_device(txt, dev)
     chunk = _lib.TRAIN_CHUNK if mode == 0 else _lib.DECODE_CHUNK
     cap = None
-    while True:
+    for _ in range(2):
         packed, res = D.ingest(ctx, d_txt, len(txt), mode, True, cap_bases=cap)
         torch.cuda.synchronize()
         ctx.sync()
@@ -57,6 +57,7 @@ def _ingest(ctx: Context, path: str, mode: int):
         if r[1] != _lib.CPG_E_CAPACITY:
             break
         # the training reader's extra all-A chunks outnumbered the default slack: size exactly
+        # (valid bases + extra chunks, both reported by the first pass)
         cap = ((r[3] // chunk) + r[4] + 2) * chunk
     if r[1] not in (_lib.CPG_OK, _lib.CPG_E_REF_CRASH):
         raise _lib.CpgError(r[1], f"device ingest of {path} failed (status {r[1]})")
@@ -82,7 +83,7 @@ def test_model(ctx: Context, model: HmmModel, test_path: str, islands_out: str, 
     log("INFO: testing")                                         # :228
     packed, nbases, r = _ingest(ctx, test_path, 1)
     cap = 1 << 16
-    while True:
+    for _ in range(2):   # (a second pass sized by the first pass's exact count)
         _, _, out, cnt = D.decode(ctx, model, packed, nbases, _lib.DECODE_CHUNK, cap=cap)
         torch.cuda.synchronize()
         ctx.sync()
