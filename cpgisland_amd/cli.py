@@ -27,7 +27,6 @@ from __future__ import annotations
 
 import sys
 
-import numpy as np
 
 from . import _lib, baumwelch
 from .hmm import Context, HmmModel, format_islands, format_model
