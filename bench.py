@@ -175,6 +175,34 @@ def _cpu_model():
     return None
 
 
+def warm_up(step_fn, args, dist, dev):
+    """The untimed warm-up: args.warmup steps, then — until args.settle_ms of wall time have
+    passed since the warm-up began — more untimed steps, in batches of 10.  A GPU that has been
+    idle runs its first ~150 steps of sustained load at lower clocks: at the driver's
+    `--warmup 5` the timed steps read 0.18 ms against 0.156 ms over 400 steps (DESIGN.md 5,
+    profiles/r03_settle).  Every rank runs the same number of steps (the steps hold
+    collectives): rank 0's clock decides, per batch.  step_fn(i) runs warm-up step i; returns
+    the count run."""
+    t0 = time.perf_counter()
+    for w in range(args.warmup):
+        step_fn(w)
+    torch.cuda.synchronize()
+    done = args.warmup
+    while args.settle_ms > 0 and done < args.warmup + 10000:
+        more = (time.perf_counter() - t0) * 1e3 < args.settle_ms
+        if dist:
+            t = torch.tensor([1 if more else 0], dtype=torch.int64, device=dev)
+            torch.distributed.broadcast(t, 0)
+            more = bool(t.item())
+        if not more:
+            break
+        for w in range(done, done + 10):
+            step_fn(w)
+        done += 10
+        torch.cuda.synchronize()
+    return done
+
+
 C3_BASES = 3_100_000_000       # configs[2]: 3.1 Gbp hg38-sized genome over the node's GPUs
 C3_SEED = 20251015 + 2         # SURVEY §8(d): seed + config index
 
@@ -354,16 +382,14 @@ def run_c3(args, world, rank, local, dist, backend, dev):
                 _gather0(iout[b], world, rank, backend, gat_i[b])
             ev["isl"][b].record(s_isl)
 
-    for w in range(args.warmup):
-        step(w, False)
-    torch.cuda.synchronize()
+    nwarm = warm_up(lambda w: step(w, False), args, dist, dev)
     ctx.sync(None)
     if dist:
         torch.distributed.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for it in range(args.steps):
-        step(args.warmup + it, True)
+        step(nwarm + it, True)
     issue = time.perf_counter() - t0
     torch.cuda.synchronize()
     if dist:
@@ -376,7 +402,7 @@ def run_c3(args, world, rank, local, dist, backend, dev):
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
-    last = (args.warmup + args.steps - 1) & 1
+    last = (nwarm + args.steps - 1) & 1
     counts = [int(c.item()) for c in gat_c[last]] if (rank == 0 and world > 1) else \
         [int(icnt[last].item())]
     if max(counts) > icap:
@@ -387,7 +413,8 @@ def run_c3(args, world, rank, local, dist, backend, dev):
         bpb = BYTES_PER_BASE["estep"] + 0.125
         ach = bpb * tr_n / (tr_ms / 1e3) / 1e9 if tr_ms > 0 else 0.0
         out = {"metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
-               "steps": args.steps, "warmup": args.warmup, "ms_per_step": ms,
+               "steps": args.steps, "warmup": args.warmup, "warmup_steps_run": nwarm,
+               "settle_ms": args.settle_ms, "ms_per_step": ms,
                "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
                "dtype": "f64", "data": f"synthetic (counter-based planted-island genome, seed {C3_SEED})",
                "config": {"workload": f"C3: {G / 1e9:.1f} Gbp hg38-sized genome split over "
@@ -418,6 +445,11 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=400)
     ap.add_argument("--warmup", type=int, default=20)
+    ap.add_argument("--settle-ms", type=float, default=100.0,
+                    help="untimed warm-up lasts at least this long: after the --warmup steps, "
+                         "more untimed steps until about this much wall time has passed (an "
+                         "idle GPU's clocks rise over its first ~25 ms of load; the count run is "
+                         "reported as warmup_steps_run; 0 = exactly --warmup steps)")
     ap.add_argument("--bases", type=int, default=N_PER_GPU,
                     help="bases per GPU (C2), or the whole genome with --workload c3 "
                          "(default there: 3.1e9)")
@@ -743,11 +775,11 @@ def main():
             main_s.wait_stream(s_dec)
             main_s.wait_stream(ln["s_red"])
 
-    for w in range(args.warmup):
+    def warm_step(w):
         step(None, w)
         if flush is not None:
             flush.fill_(1.0)
-    torch.cuda.synchronize()
+    nwarm = warm_up(warm_step, args, dist, dev)
     for ln in lanes:
         ln["ctx"].sync(None)
     if dist:
@@ -765,7 +797,7 @@ def main():
     for it in range(args.steps):
         if flush is not None:
             flush.fill_(1.0)
-        step(it, it)
+        step(it, nwarm + it)
     issue = time.perf_counter() - t0   # host time to enqueue every step (launch-bound check)
     tl = [("issued", issue)]
     # the end of the timed region: one device-wide synchronize waits for every stream of
@@ -864,7 +896,8 @@ def main():
             "unit": "GB/s", "frac": None}
         roof_decode["frac"] = round(roof_decode["achieved"] / HBM_PEAK_GBS, 4)
         out = {"metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
-               "steps": steps, "warmup": args.warmup, "ms_per_step": ms_per_step,
+               "steps": steps, "warmup": args.warmup, "warmup_steps_run": nwarm,
+               "settle_ms": args.settle_ms, "ms_per_step": ms_per_step,
                "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
                "dtype": "f64", "data": "synthetic (counter-based planted-island genome, "
                                         f"seed {SEED})",
