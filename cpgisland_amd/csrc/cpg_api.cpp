@@ -103,9 +103,13 @@ int vit_tables(cpg_ctx* ctx, const cpg_model* m, const VitConsts& vc, const VitT
     return CPG_OK;
 }
 
-// the E-step's one-step tables, cached per model like the Viterbi tables: rows
+// the E-step's tables, cached per model like the Viterbi tables: one-step rows
 // TA[d] = (a[p][b], a[p][b+4]), TB[d] = (a[p+4][b], a[p+4][b+4]) for d = p | b << 2 (p the
-// previous base, b the current one) — written once per model instead of a kernel per call
+// previous base, b the current one); then the two-step rows of the trinucleotide keys
+// tau = x0 | x1 << 2 | x2 << 4, P_tau = M_{x0 x1} M_{x1 x2} (T2A: row +, T2B: row -), and
+// keys 64 + d = the one-step M_d (k_estep.hip 3b) — written once per model
+constexpr int kEstKeys = 80;
+constexpr int kEstTabRows = 32 + 2 * kEstKeys;
 int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out) {
     for (int i = 0; i < ctx->etn; ++i)
         if (std::memcmp(&ctx->etc_[i].model, m, sizeof *m) == 0) {
@@ -115,17 +119,31 @@ int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out) {
     cpg_ctx::EtSlot* sl;
     if (ctx->etn < cpg_ctx::kVtSlots) {
         sl = &ctx->etc_[ctx->etn++];
-        CPG_HIP(hipMalloc(&sl->d, 32 * sizeof(double2)));
+        CPG_HIP(hipMalloc(&sl->d, kEstTabRows * sizeof(double2)));
     } else {
         sl = &ctx->etc_[ctx->etnext];
         ctx->etnext = (ctx->etnext + 1) % cpg_ctx::kVtSlots;
         CPG_HIP(hipDeviceSynchronize());   // the evicted slot may still be read
     }
-    double2 h[32];
+    double2 h[kEstTabRows];
+    auto M = [&](int d, int s, int s2) { return m->a[(d & 3) + 4 * s][(d >> 2) + 4 * s2]; };
     for (int d = 0; d < 16; ++d) {
-        const int p = d & 3, b = d >> 2;
-        h[d] = make_double2(m->a[p][b], m->a[p][b + 4]);
-        h[16 + d] = make_double2(m->a[p + 4][b], m->a[p + 4][b + 4]);
+        h[d] = make_double2(M(d, 0, 0), M(d, 0, 1));
+        h[16 + d] = make_double2(M(d, 1, 0), M(d, 1, 1));
+    }
+    for (int k = 0; k < kEstKeys; ++k) {
+        double P[2][2];
+        for (int s = 0; s < 2; ++s)
+            for (int s2 = 0; s2 < 2; ++s2) {
+                if (k >= 64) {
+                    P[s][s2] = M(k - 64, s, s2);
+                } else {
+                    const int d1 = k & 15, d2 = k >> 2;
+                    P[s][s2] = M(d1, s, 0) * M(d2, 0, s2) + M(d1, s, 1) * M(d2, 1, s2);
+                }
+            }
+        h[32 + k] = make_double2(P[0][0], P[0][1]);
+        h[32 + kEstKeys + k] = make_double2(P[1][0], P[1][1]);
     }
     sl->model = *m;
     CPG_HIP(hipMemcpy(sl->d, h, sizeof h, hipMemcpyHostToDevice));

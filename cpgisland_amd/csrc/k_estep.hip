@@ -38,21 +38,26 @@ namespace {
 
 constexpr int kET = 1024;               // max lanes per chunk
 constexpr int kLanePos = 64;            // positions per lane
-constexpr int kSlab = 73;               // trans[64] (by dinucleotide x 4) | init[8] | loglik
+// accumulator slab: class bins trans[64] (by dinucleotide x 4) | init[8] | loglik, then the
+// two-position blocks' key bins [64 keys][4] (see 3b)
+constexpr int kSlabCls = 73;
+constexpr int kKeys = 80;               // 64 trinucleotides + 16 one-step keys (lane 0's first block)
+constexpr int kKeyRows = 64 * 4;        // LDS bin rows / key accumulators (one-step keys: direct)
+constexpr int kSlab = kSlabCls + kKeyRows;
 // workgroups add into kAccRep replicated accumulator sets (chosen by chunk index) so that
 // ~700 workgroups do not serialise on 73 device-scope atomic addresses; the finalize sums
 // the replicas in 128-bit integer arithmetic (exact, order-independent)
 constexpr int kAccRep = 16;
-// xi bins: ONE set of 64 rows (k = pair, d = class: row k * 16 + d) x 16 columns (u64), lane
-// column = lane % 16.  An LDS 64-bit access serves 16 lanes per cycle with bank = (address /
+// bins: ONE set of 256 rows (row = key * 4 + pair) x 16 columns (u64), lane column = lane % 16.  An LDS 64-bit access serves 16 lanes per cycle with bank = (address /
 // 4) mod 32: the 16 lanes of a pass always hit 16 different columns = 32 different banks,
 // whatever their classes — no bank conflicts and no same-address collisions inside a pass
 // (per-wave replicated sets, measured earlier, collide whenever two lanes of a pass share a
 // class).
-// LDS: TA/TB (512 B) | union { 4-step tables, scan buffer, bins } | per-wave partials
-constexpr size_t kUnionOff = 32 * 16;
+// LDS: TA/TB (512 B) | T2A/T2B (2.5 KB) | union { 4-step tables, scan buffer, bins } |
+// epilogue scratch | alpha checkpoints
+constexpr size_t kUnionOff = (32 + 2 * kKeys) * 16;
 constexpr size_t kUnionBytes = 2048 * 16;
-__device__ __forceinline__ int bin_of(int d, int k) { return k * 16 + d; }
+static_assert(kKeyRows * 16 * 8 <= kUnionBytes, "bins fit the union");
 
 struct Mat {
     double a, b, c, d;   // [[a b] [c d]]
@@ -270,7 +275,8 @@ __device__ __forceinline__ unsigned long long xor_te(unsigned long long v, int t
 }
 
 template <bool kAgent>
-__device__ void finalize(unsigned long long* acc, double* vsum, double* out);
+__device__ void finalize(const cpg_model& model, unsigned long long* acc, double* vsum,
+                         double* out);
 __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 
 // waves per SIMD: the workgroup's 16 waves take 4 per SIMD; with <= 96 VGPRs (5 per SIMD) a
@@ -297,7 +303,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     double2* TB = TA + 16;                                    // (M(-,+), M(-,-))
     // one union region after TA/TB, used in turn by: the 4-step tables (phase 1), the scan
     // buffer (phase 2), the xi bins (phase 3) — each phase ends with a barrier
-    double2* TA4 = TB + 16;                                   // 4-step products, row 0
+    double2* T2A = TB + 16;                                   // 2-step (P(+,+), P(+,-))
+    double2* T2B = T2A + kKeys;                               // 2-step (P(-,+), P(-,-))
+    double2* TA4 = reinterpret_cast<double2*>(smem + kUnionOff);   // 4-step products, row 0
     auto* part = reinterpret_cast<unsigned long long*>(
         smem + kUnionOff + kUnionBytes);
     double2* fck = reinterpret_cast<double2*>(part + 16 * 64);   // [NMB][nl] alpha checkpoints
@@ -308,9 +316,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     const int lane = t & 63;
     const int64_t c = blockIdx.x;
     const uint32_t* pk = packed + c * (C / 16);
-    // the one-step rows from the model's cached table (est_tables: L2-resident, 512 B)
+    // the one- and two-step rows from the model's cached table (est_tables: L2-resident, 3 KB)
     // rather than per-lane reads of the kernel-argument model
-    if (t < 32) TA[t] = gtab[t];   // TB = TA + 16
+    for (int i = t; i < 32 + 2 * kKeys; i += nl) TA[i] = gtab[i];   // TB, T2A, T2B follow TA
     const Codes cd0 = lane_codes(pk, t);   // (in flight across the barrier)
     // fused counts: the workgroup's 72 count sums (LDS atomics) and the finalize's raw sums
     // in the epilogue scratch `part` (free until the epilogue's first 76 words)
@@ -485,172 +493,155 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
 
     // 3a. bins (aliasing the scan buffer, read above) zeroed; alpha entering mini-block m
     //     = alpha entering the lane times phase 1's product of the first m mini-blocks
-    //     (any per-position scale cancels in the normalised xi)
-    for (int i = t; i < 64 * 16; i += nl) bins[i] = 0ull;
+    //     (any per-position scale cancels in the normalised posteriors)
+    for (int i = t; i < kKeyRows * 16; i += nl) bins[i] = 0ull;
     __syncthreads();
-    // 3b. mini-blocks, last to first: forward alphas in registers from the checkpoint, then
-    //     backward with xi accumulation; beta flows on from one mini-block to the previous
+    // 3b. mini-blocks, last to first, in TWO-POSITION BLOCKS: block j of a mini-block is its
+    //     positions (2j, 2j+1), keyed by the trinucleotide tau = (x_{2j-1}, x_{2j}, x_{2j+1})
+    //     and stepped by the 2-step matrix P_tau = M_{2j} M_{2j+1} (T2A/T2B).  Forward: the
+    //     alphas A_j = alpha_{2j-1} of the 8 blocks in registers (the whole mini-block: no
+    //     second forward pass).  Backward: beta pre-scaled by 2^47 / Z as in one-step form —
+    //     A_j . (P_tau y_{2j+1}) = 2^47 at every block — so the joint posterior of the states
+    //     at 2j-1 and 2j+1,  Zeta(a,c) * 2^47 = A_j(a) * (P_tau(a,c) y(c)),  is one fma onto
+    //     the fixed-point grid; both positions' pair posteriors are exact linear images of it
+    //     (xi_{2j}(a,b) = sum_c f(a,b,c) Zeta(a,c), xi_{2j+1}(b,c) = sum_a f(a,b,c) Zeta(a,c),
+    //     f(a,b,c) = M(a,b) M(b,c) / P(a,c): the share of the paths a -> c through b), applied
+    //     once to the exact integer sums in the finalize.  4 LDS atomics per TWO positions,
+    //     one table row pair per two positions each way, ~half the fp64 of one-step form.
+    //     Lane 0's first block holds position 1 alone (position 0 carries no transition): its
+    //     key 64 + class(x0, x1) selects the one-step matrix, its Zeta IS xi_1 (added to the
+    //     class accumulators directly) and it ends with gamma_0 (the init posteriors).
     unsigned long long* wb = bins + (lane & 15);
     constexpr int kBS = 16;   // row stride
+    const double2* __restrict__ g2a = gtab + 32;          // backward rows (global, L1-resident)
+    const double2* __restrict__ g2b = gtab + 32 + kKeys;
     double yP = bP, yM = bM;   // beta at the last position of the mini-block
-    // (measured and dropped: mini-block m's backward pass interleaved with mini-block m-1's
-    // forward pass, two dependency chains per wave — 16 alpha pairs live either way, but the
-    // two chains' temporaries spill: 0.18 vs 0.127 ms)
+#pragma unroll 1
     for (int m = NMB - 1; m >= 0; --m) {
-        // the mini-block's codes from its packed word (L1/L2, two dwords): neither 8 live
-        // VGPRs of codes nor a scratch copy of them
+        // the mini-block's bases from its packed word and the last base of the word before:
+        // base q at bits 2q+2 of cm, base -1 at bits 0-1; block j's key = bits 4j .. 4j+5
         const uint32_t xw = pk[4 * t + m];
         const uint32_t pw = (t > 0 || m > 0) ? pk[4 * t + m - 1] : 0u;
-        const uint64_t cm = codes16(xw, pw >> 30);
-        // alpha at the position before the mini-block (its checkpoint)
-        const double2 f = fck[m * nl + t];
-        const double bfP = f.x, bfM = f.y;
-        // alpha registers hold one half of the mini-block: the second half's alphas from a
-        // forward pass over all 16 positions, then (after its backward pass) the first half's
-        // from a second forward pass — 32 fewer VGPRs than the whole mini-block's, for 2 extra
-        // fp64 per position, so that the kernel fits 5 waves per SIMD (see kWavesPerEU)
-        constexpr int kH = kMB / 2;
-        double alP[kH], alM[kH];
-        double hP = bfP, hM = bfM;   // alpha at position lo - 1 (the position before the half)
-        int kf[kMB / 4];   // alpha's power-of-two shifts at positions 3, 7, 11, 15
-        auto forward = [&](int lo, int hi) {   // positions [0, hi); alphas of [lo, hi) kept
-            double xP = bfP, xM = bfM;
-#pragma unroll
-            for (int i = 0; i < hi; ++i) {
-                if (!(t == 0 && m == 0 && i == 0)) {   // (alpha_0 itself at the chunk start)
-                    const uint32_t d = code_at(cm, i);
-                    const double2 ma = TA[d], mb = TB[d];
-                    const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
-                    xP = nP;
-                    xM = nM;
-                    if ((i & 3) == 3) kf[i >> 2] = vnorm(xP, xM);
-                }
-                if (i == lo - 1) {
-                    hP = xP;
-                    hM = xM;
-                }
-                if (i >= lo) {
-                    alP[i - lo] = xP;
-                    alM[i - lo] = xM;
-                }
-            }
+        const uint64_t cm = ((uint64_t)xw << 2) | (pw >> 30);
+        const bool sp = t == 0 && m == 0;
+        auto key = [&](int j) -> uint32_t {   // j compile-time
+            const uint32_t k = (uint32_t)(cm >> (4 * j)) & 63u;
+            return (j == 0 && sp) ? 64u + (k >> 2) : k;
         };
-        // beta pre-scaled by 2^47 / Z: with a_i = the stored (renormalised) alpha at i and
-        // s_i its shift (a_{i-1} M_i = 2^{s_i} a_i), keep  a_{i-1} . (M_i y_i) = 2^47  at
-        // every position, so xi_i(a,b) * 2^47 = a_{i-1}(a) * (M_i(a,b) y_i(b)) — one fma per
-        // pair, straight onto the fixed-point grid (fma(., ., 1.5*2^52)), no per-position
-        // normaliser.  Start: y_15 = beta_15 * 2^{47-s_15} / (a_15 . beta_15); crossing an
-        // alpha renormalisation point going backward (i-1 = 11, 7, 3) scales y by 2^{-s}.
-        // y only shrinks through M (entries <= 1) and grows by the alpha shifts of one
-        // mini-block; it is renormalised once per mini-block.
-        auto bstart = [&]() {
-            vnorm(yP, yM);
-            const double r =
-                ldexp(rcp_nr(alP[kH - 1] * yP + alM[kH - 1] * yM), 47 - kf[kMB / 4 - 1]);
+        const double2 f = fck[m * nl + t];   // alpha at the position before the mini-block
+        constexpr int kB = kMB / 2;          // blocks per mini-block
+        double alP[kB], alM[kB];
+        int kf[kB / 2];   // alpha's power-of-two shifts at positions 3, 7, 11, 15 (A_2,4,6,8)
+        double xP = f.x, xM = f.y;
+#pragma unroll
+        for (int j = 0; j < kB; ++j) {
+            alP[j] = xP;
+            alM[j] = xM;
+            const uint32_t k = key(j);
+            const double2 ma = T2A[k], mb = T2B[k];
+            const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
+            xP = nP;
+            xM = nM;
+            if (j & 1) kf[j >> 1] = vnorm(xP, xM);
+        }
+        // y_15 = beta_15 * 2^{47 - s_15} / (A_8 . beta_15)  (A_8 = alpha_15 after its shift)
+        vnorm(yP, yM);
+        {
+            const double r = ldexp(rcp_nr(xP * yP + xM * yM), 47 - kf[kB / 2 - 1]);
             yP *= r;
             yM *= r;
-        };
-constexpr int kPFD = 1;   // backward table rows loaded this many positions ahead (2, 3: no faster)
-        // the backward pass's table rows come from a global copy (L1-resident): waited on
-        // with vmcnt, not behind the preceding LDS atomics (LDS operations retire in order;
-        // an LDS copy read ahead of the atomics spills)
-        auto backward = [&](int lo, int hi) {   // positions hi - 1 .. lo
-            double2 qa[kPFD + 1], qb[kPFD + 1];
-            auto trow = [&](int i, double2& a, double2& b) {
-                const uint32_t d = code_at(cm, i);
-                a = gtab[d];
-                b = gtab[16 + d];
-            };
+        }
+        constexpr int kPFD = 1;   // backward rows loaded this many blocks ahead
+        double2 qa[kPFD + 1], qb[kPFD + 1];
 #pragma unroll
-            for (int j = 0; j < kPFD; ++j) trow(hi - 1 - j, qa[j], qb[j]);
+        for (int j = 0; j < kPFD; ++j) {
+            const uint32_t k = key(kB - 1 - j);
+            qa[j] = g2a[k];
+            qb[j] = g2b[k];
+        }
 #pragma unroll
-            for (int i = hi - 1; i >= lo; --i) {
-                // table rows issued kPFD positions ahead; the scheduling barrier keeps the
-                // compiler from sinking them to their use, which had put one full L1/L2 round
-                // trip (two, serialised) on every position's chain
-                if (i - kPFD >= lo)
-                    trow(i - kPFD, qa[(hi - 1 - i + kPFD) % (kPFD + 1)],
-                         qb[(hi - 1 - i + kPFD) % (kPFD + 1)]);
-                __builtin_amdgcn_sched_barrier(0);
-                const uint32_t d = code_at(cm, i);
-                const double2 ma = qa[(hi - 1 - i) % (kPFD + 1)],
-                              mb = qb[(hi - 1 - i) % (kPFD + 1)];
-                if (t == 0 && m == 0 && i == 0) {   // gamma_0 = a_0 * y_0 / 2^47 -> init counts,
-                    // added at once (nothing stays live across the main loop for it)
-                    const uint32_t b0 = pk[0] & 3u;
-                    unsigned long long* ra = acc + 2 * kSlab * (c % kAccRep);
-                    acc128_add(ra + 2 * (64 + b0), to_fixed_init(alP[0] * yP), false);
-                    acc128_add(ra + 2 * (64 + b0 + 4), to_fixed_init(alM[0] * yM), false);
-                    continue;
-                }
-                const double uP = i > lo ? alP[i - 1 - lo] : (lo > 0 ? hP : bfP);
-                const double uM = i > lo ? alM[i - 1 - lo] : (lo > 0 ? hM : bfM);
-                // M y products, shared by the pair marginals and the beta update
-                const double t00 = ma.x * yP, t01 = ma.y * yM, t10 = mb.x * yP, t11 = mb.y * yM;
-                atomicAdd(wb + bin_of(d, 0) * kBS, raw_fma(uP, t00));
-                atomicAdd(wb + bin_of(d, 1) * kBS, raw_fma(uP, t01));
-                atomicAdd(wb + bin_of(d, 2) * kBS, raw_fma(uM, t10));
-                atomicAdd(wb + bin_of(d, 3) * kBS, raw_fma(uM, t11));
-                yP = t00 + t01;
-                yM = t10 + t11;
-                if (i == 4 || i == 8 || i == 12) {
-                    yP = ldexp(yP, -kf[(i - 1) >> 2]);
-                    yM = ldexp(yM, -kf[(i - 1) >> 2]);
-                }
+        for (int j = kB - 1; j >= 0; --j) {
+            // rows issued kPFD blocks ahead; the scheduling barrier keeps the compiler from
+            // sinking them to their use (one L1/L2 round trip on every block's chain)
+            if (j - kPFD >= 0) {
+                const uint32_t k = key(j - kPFD);
+                qa[(kB - 1 - j + kPFD) % (kPFD + 1)] = g2a[k];
+                qb[(kB - 1 - j + kPFD) % (kPFD + 1)] = g2b[k];
             }
-        };
-        forward(kH, kMB);
-        bstart();
-        backward(kH, kMB);
-        forward(0, kH);
-        backward(0, kH);
+            __builtin_amdgcn_sched_barrier(0);
+            const uint32_t k = key(j);
+            const double2 ma = qa[(kB - 1 - j) % (kPFD + 1)], mb = qb[(kB - 1 - j) % (kPFD + 1)];
+            // P y products, shared by the joint posteriors and the beta update
+            const double t00 = ma.x * yP, t01 = ma.y * yM, t10 = mb.x * yP, t11 = mb.y * yM;
+            if (j == 0 && sp) {   // xi_1 and gamma_0, added at once to the class and init
+                                  // accumulators (nothing stays live across the main loop)
+                const uint32_t d = k - 64u;
+                acc128_add(racc + 2 * (d * 4 + 0), to_fixed_scaled(alP[0] * t00), false);
+                acc128_add(racc + 2 * (d * 4 + 1), to_fixed_scaled(alP[0] * t01), false);
+                acc128_add(racc + 2 * (d * 4 + 2), to_fixed_scaled(alM[0] * t10), false);
+                acc128_add(racc + 2 * (d * 4 + 3), to_fixed_scaled(alM[0] * t11), false);
+                const uint32_t b0 = xw & 3u;
+                acc128_add(racc + 2 * (64 + b0), to_fixed_init(alP[0] * (t00 + t01)), false);
+                acc128_add(racc + 2 * (64 + b0 + 4), to_fixed_init(alM[0] * (t10 + t11)), false);
+            } else {
+                unsigned long long* row = wb + (int)k * (4 * kBS);
+                atomicAdd(row + 0 * kBS, raw_fma(alP[j], t00));
+                atomicAdd(row + 1 * kBS, raw_fma(alP[j], t01));
+                atomicAdd(row + 2 * kBS, raw_fma(alM[j], t10));
+                atomicAdd(row + 3 * kBS, raw_fma(alM[j], t11));
+            }
+            yP = t00 + t01;
+            yM = t10 + t11;
+            if (j == 2 || j == 4 || j == 6) {   // crossing A_j's renormalisation point
+                yP = ldexp(yP, -kf[j / 2 - 1]);
+                yM = ldexp(yM, -kf[j / 2 - 1]);
+            }
+        }
     }
     __syncthreads();
     // the epilogue's indices from an opaque copy of the thread index: the compiler would
     // otherwise keep the prologue's (shuffle) indices live across the main loop, in scratch
     int te = threadIdx.x;
     asm volatile("" : "+v"(te));
-    // chunk totals: row te = d * 4 + k, the sum of its 16 columns (integer: exact in any order)
-    if (te < 64) {
-        const unsigned long long* row = bins + bin_of(te >> 2, te & 3) * 16;
+    // chunk totals: row te = key * 4 + (2a + c), the sum of its 16 columns (integer: exact in
+    // any order); the key's 4 raw sums (lanes 4 key .. 4 key + 3 of one wave) -> its block
+    // count -> K removed -> the key accumulators (slots kSlabCls + row)
+    for (int r = te; r < kKeyRows; r += nl) {   // (nl: a multiple of 64)
+        const unsigned long long* row = bins + r * 16;
         unsigned long long s = 0;
 #pragma unroll
-        for (int col = 0; col < 16; ++col) s += row[(col + te) & 15];   // rotated: no conflicts
-        part[te] = s;
-    }
-    __syncthreads();
-    // chunk results -> the global 128-bit accumulators: xi bins and the init posteriors in
-    // 2^-47 units, the log-likelihood in signed 2^-24 units
-    if (te < 64) {   // row te = d * 4 + k (wave 0)
-        unsigned long long s = part[te];
-        // the class's 4 raw sums (lanes 4d .. 4d+3) -> its position count -> K removed
+        for (int col = 0; col < 16; ++col) s += row[(col + r) & 15];   // rotated: no conflicts
         unsigned long long S = s;
         S += xor_te(S, te, 1);   // (lane addresses from te, see above)
         S += xor_te(S, te, 2);
         s -= class_count(S) * kMagicBits;
-        acc128_add(racc + 2 * te, s, false);
+        if (s) acc128_add(racc + 2 * (kSlabCls + r), s, false);
     }
-    if (kCnt && te >= 64 && te < 64 + cnt::kRaw) {   // waves 1-2: the count sums
-        const uint32_t v = cnt::raw_of(scnt, te - 64);
-        if (v) atomicAdd(cacc + (c % cnt::kRep) * cnt::kRaw + (te - 64), (unsigned long long)v);
+    if (kCnt && te < cnt::kRaw) {   // the count sums (kCnt: >= 256 lanes)
+        const uint32_t v = cnt::raw_of(scnt, te);
+        if (v) atomicAdd(cacc + (c % cnt::kRep) * cnt::kRaw + te, (unsigned long long)v);
     }
     // done != nullptr: the last workgroup to finish converts the sums (one launch per call)
     if (done && last_workgroup(done, reinterpret_cast<int*>(part))) {
         // the count replicas are read by waves 2-3 beside the E-step's (finalize's barrier)
         uint64_t* craw = reinterpret_cast<uint64_t*>(part + 192);
         if (kCnt && te >= 128 && te < 128 + cnt::kRaw) cnt::fin_load<true>(cacc, craw, te - 128);
-        finalize<true>(acc, reinterpret_cast<double*>(part + 2), out);
+        finalize<true>(model, acc, reinterpret_cast<double*>(part + 512), out);
         if (kCnt) cnt::fin_store(cacc, craw, cout, te, nl);
         reset_done(done);
     }
 }
 
 
-// The 73 accumulators (replicas summed in 128-bit integer arithmetic) -> doubles, re-zeroed
-// for the next call, then the cpg_counts_f64 assembly.  kAgent: written by workgroups of the
-// same launch (device-scope loads).
+// The accumulators (replicas summed in 128-bit integer arithmetic) -> doubles, re-zeroed
+// for the next call; the key bins of the two-position blocks mapped onto the class bins
+// (k_estep_chunk 3b: xi_{2j}(a,b) = sum_c f Zeta(a,c), xi_{2j+1}(b,c) = sum_a f Zeta(a,c)
+// with f(a,b,c) = M1(a,b) M2(b,c) / sum_b' M1(a,b') M2(b',c), M1 / M2 the one-step matrices
+// of the key's two classes); then the cpg_counts_f64 assembly.  kAgent: written by
+// workgroups of the same launch (device-scope loads).
 template <bool kAgent>
-__device__ void finalize(unsigned long long* acc, double* vsum, double* out) {
+__device__ void finalize(const cpg_model& model, unsigned long long* acc, double* vsum,
+                         double* out) {
     const int t = threadIdx.x;
     for (int i = t; i < kSlab; i += blockDim.x) {
         unsigned long long lo = 0ull, hi = 0ull;   // 128-bit sum of the replicas
@@ -669,19 +660,46 @@ __device__ void finalize(unsigned long long* acc, double* vsum, double* out) {
         }
         const double mag = (double)hi * 18446744073709551616.0 + (double)lo;
         vsum[i] = i < 64 ? mag * (1.0 / kFix)
-                : i < 72 ? mag * (1.0 / kFixInit) : ldexp(neg ? -mag : mag, -kLogFix);
+                : i < 72 ? mag * (1.0 / kFixInit)
+                : i == 72 ? ldexp(neg ? -mag : mag, -kLogFix) : mag * (1.0 / kFix);
     }
     __syncthreads();
     for (int i = t; i < 2 * kSlab * kAccRep; i += blockDim.x) acc[i] = 0ull;
+    double xs = 0.0;
+    if (t < 64) {   // class bin t = d * 4 + 2a + b
+        const int d = t >> 2, a = (t >> 1) & 1, b = t & 1;
+        // M_e(s, s') = a[p + 4s][q + 4s'], e = p | q << 2 (p the previous base, q the current)
+        auto M = [&](int e, int s, int s2) { return model.a[(e & 3) + 4 * s][(e >> 2) + 4 * s2]; };
+        auto share = [&](int d1, int d2, int x, int y, int z) {   // f(x, y, z)
+            const double w0 = M(d1, x, 0) * M(d2, 0, z), w1 = M(d1, x, 1) * M(d2, 1, z);
+            const double w = w0 + w1;
+            return w > 0.0 ? (y ? w1 : w0) / w : 0.0;
+        };
+        const double* zk = vsum + kSlabCls;
+        for (int r = 0; r < 4; ++r) {   // keys whose first position has class d: (a, b) first
+            const int key = d | (r << 4), d2 = key >> 2;
+            for (int cc = 0; cc < 2; ++cc)
+                xs += share(d, d2, a, b, cc) * zk[key * 4 + 2 * a + cc];
+        }
+        for (int p = 0; p < 4; ++p) {   // keys whose second position has class d: (a, b) second
+            const int key = p | (d << 2), d1 = key & 15;
+            for (int aa = 0; aa < 2; ++aa)
+                xs += share(d1, d, aa, a, b) * zk[key * 4 + 2 * aa + b];
+        }
+    }
+    __syncthreads();
+    if (t < 64) vsum[t] += xs;
+    __syncthreads();
     for (int i = t; i < 105; i += blockDim.x) final_estep(vsum, i, out);
 }
 
 // One workgroup: finalize of accumulators filled by earlier launches (streamed genome,
 // contig batches).
-__global__ __launch_bounds__(256) void k_estep_final(unsigned long long* __restrict__ acc,
+__global__ __launch_bounds__(256) void k_estep_final(const cpg_model model,
+                                                     unsigned long long* __restrict__ acc,
                                                      double* __restrict__ out) {
     __shared__ double vsum[kSlab];
-    finalize<false>(acc, vsum, out);
+    finalize<false>(model, acc, vsum, out);
 }
 
 // cpg_counts_f64 from the 73 sums: init[8] trans[8][8] emit[8][4] loglik; thread t < 105
@@ -737,7 +755,7 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
         if (done) return hipGetLastError();
     }
     if (parts & PART_FINAL)
-        hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, acc, out);
+        hipLaunchKernelGGL(k_estep_final, dim3(1), dim3(256), 0, s, model, acc, out);
     return hipGetLastError();
 }
 

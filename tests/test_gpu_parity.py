@@ -537,9 +537,12 @@ def test_estep_trained_model_iteration(gpu_ctx, torch_dev):
 
 def estep_grid_bound(obs, chunk_len):
     """Absolute error bound, per cpg_counts_f64 entry, of the E-step kernel's fixed-point sums
-    (k_estep.hip): every pair posterior xi is rounded to the nearest multiple of 2^-47 before
-    it is summed exactly, so a transition bin of class d (previous base | current base << 2)
-    is off by at most n_d * 2^-48, n_d = the positions of class d over the whole chunks; an
+    (k_estep.hip): positions go in two-position blocks whose 4 joint posteriors Zeta(a,c) are
+    each rounded to the nearest multiple of 2^-47 (error <= 2^-48) before they are summed
+    exactly; each position's pair posterior xi is a convex-weighted sum of two of them
+    (xi_{2j}(a,b) = sum_c f(a,b,c) Zeta(a,c), f <= 1), so a transition bin of class d (previous
+    base | current base << 2) is off by at most n_d * 2^-47, n_d = the positions of class d
+    over the whole chunks; an
     emission entry (init + a column of transition bins) by the sum of its terms' bounds; the
     init posteriors (2^-62 grid) by 2^-63 per chunk; the log-likelihood (2^-24 per chunk) by
     2^-25 per chunk.  The fp64 arithmetic itself (a different association than the oracle's)
@@ -553,7 +556,7 @@ def estep_grid_bound(obs, chunk_len):
     b[:8] = nch * 2.0 ** -63
     for i in range(8):
         for j in range(8):
-            b[8 + 8 * i + j] = nd[(i & 3) | ((j & 3) << 2)] * 2.0 ** -48
+            b[8 + 8 * i + j] = nd[(i & 3) | ((j & 3) << 2)] * 2.0 ** -47
     for j in range(8):
         b[72 + 4 * j + (j & 3)] = b[j] + sum(b[8 + 8 * i + j] for i in range(8))
     b[104] = nch * 2.0 ** -25
@@ -588,7 +591,7 @@ def test_estep_single_class_chunks(gpu_ctx, torch_dev):
         got = D.bw_estep(gpu_ctx, _model(m), dp, n, TRAIN).cpu().numpy()
         ref = co.estep(m, obs, TRAIN)
         # the '+' posteriors of these chunks are far below the 2^-47 grid: their bins are
-        # within the grid's derived bound (n_d * 2^-48), every other entry within 1e-9
+        # within the grid's derived bound (n_d * 2^-47), every other entry within 1e-9
         # relative; the init posteriors (2^-62 grid) within 1e-9 relative everywhere
         assert_estep_close(got, ref, obs, TRAIN, name)
         nz = ref[:8] != 0
