@@ -146,7 +146,7 @@ int est_tables(cpg_ctx* ctx, const cpg_model* m, const double2** out) {
         h[32 + kEstKeys + k] = make_double2(P[1][0], P[1][1]);
     }
     sl->model = *m;
-    CPG_HIP(hipMemcpy(sl->d, h, sizeof h, hipMemcpyHostToDevice));
+    CPG_HIP(hipMemcpy(sl->d, h, sizeof(double2) * kEstTabRows, hipMemcpyHostToDevice));
     *out = sl->d;
     return CPG_OK;
 }

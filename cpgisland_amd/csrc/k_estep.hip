@@ -342,6 +342,8 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         __builtin_amdgcn_sched_barrier(0);
     }
     // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4), from the rows
+    // (computing them here measured faster than copying a per-model table: 32 KB of L2 reads
+    // per workgroup)
     for (int i = t; i < 1024; i += nl) {
         double x00 = 1.0, x01 = 0.0, x10 = 0.0, x11 = 1.0;
 #pragma unroll
@@ -356,7 +358,6 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         TB4[i] = make_double2(x10, x11);
     }
     __syncthreads();
-
     constexpr int L = kLanePos;            // 64 positions per lane
     constexpr int kMB = 16, NMB = L / kMB;
     const int p0 = t * L;
@@ -401,9 +402,13 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         P = mmul(P, G);   // normalised
         if (g < NMB - 1) Pk[g] = make_double4(P.a, P.b, P.c, P.d);
     }
-    // 2. prefix and suffix products of the lane products: shuffle scans inside each wave
-    //    (interleaved), one wave scans the wave totals, two barriers in all
-    const int wv = t >> 6;
+    // 2. alpha entering and beta leaving every lane.  (a) prefix and suffix products of the
+    //    lane products inside each 16-lane row (DPP, identity at the row edges); (b) the 64
+    //    row totals to LDS; (c) one wave: 16 lanes form the totals of 4 rows each, scan them
+    //    (DPP) and walk their 4 rows with VECTORS — alpha entering / beta leaving every row
+    //    (one mat-vec per row, exponents tracked for the log-likelihood) — to LDS; (d) every
+    //    lane: alpha = its row's entering alpha x the row prefix before it, beta likewise.
+    //    Two barriers; no cross-row matrix shuffles.
     Mat xp = P, xs = P;
 #pragma unroll
     for (int off = 1; off < 16; off <<= 1) {   // inside rows: DPP (identity at row edges)
@@ -411,71 +416,97 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         xp = off < 8 ? mmul_nn(yp, xp) : mmul(yp, xp);
         xs = off < 8 ? mmul_nn(xs, ys) : mmul(xs, ys);
     }
-    // across rows (the LDS crossbar), the row totals: prefix — rows 1, 3 take the last lane
-    // of the row before, then rows 2, 3 take lane 31; suffix — rows 0, 2 take the first lane
-    // of the row after, then rows 0, 1 take lane 32
-    {
-        const int row = lane >> 4;
-        Mat yp = shfl_mat(xp, (lane | 15) - 16), ys = shfl_mat(xs, (lane & ~15) + 16);
-        Mat np = mmul_nn(yp, xp), ns = mmul_nn(xs, ys);
-        xp = msel(row & 1, np, xp);
-        xs = msel(!(row & 1), ns, xs);
-        yp = shfl_mat(xp, 31);
-        ys = shfl_mat(xs, 32);
-        np = mmul(yp, xp);
-        ns = mmul(xs, ys);
-        xp = msel(row >= 2, np, xp);
-        xs = msel(row < 2, ns, xs);
-    }
-    const Mat I1 = mid();
-    const Mat up1 = dpp_mat<0x138>(xp, I1), dn1 = dpp_mat<0x130>(xs, I1);   // wave_shr/shl:1
-    __syncthreads();   // every lane is past its 4-step table reads: the union is free
-    Mat* sWP = reinterpret_cast<Mat*>(uni);   // [16] wave products (prefix order)
-    Mat* sWS = sWP + 16;                      // [16] wave products (suffix order)
-    Mat* sXP = sWS + 16;                      // [17] products of the waves before; [16] all
-    Mat* sXS = sXP + 17;                      // [16] products of the waves after
-    if (lane == 63) sWP[wv] = xp;
-    if (lane == 0) sWS[wv] = xs;
-    __syncthreads();
-    if (t < 64) {
-        Mat wp = t < nw ? sWP[t] : mid(), ws = t < nw ? sWS[t] : mid();
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {   // the 16 wave totals: row 0, DPP
-            const Mat yp = row_up(wp, off), ys = row_down(ws, off);
-            wp = off < 8 ? mmul_nn(yp, wp) : mmul(yp, wp);
-            ws = off < 8 ? mmul_nn(ws, ys) : mmul(ws, ys);
-        }
-        const Mat ep = row_up(wp, 1), es = row_down(ws, 1);
-        if (t < nw) {
-            sXP[t] = t > 0 ? ep : mid();
-            sXS[t] = t + 1 < nw ? es : mid();
-        }
-        if (t == nw - 1) sXP[16] = wp;
-    }
-    __syncthreads();
+    const Mat up1 = row_up(xp, 1), dn1 = row_down(xs, 1);   // exclusive, inside the row
+    // (the scan buffer lies outside the union: no barrier for the 4-step table reads here)
+    const int nr = nl >> 4, row = t >> 4;                      // rows of 16 lanes
+    // (the epilogue scratch after the count sums; 4.6 KB)
+    Mat* sRP = reinterpret_cast<Mat*>(part + 192);             // [64] row totals
+    double2* sAR = reinterpret_cast<double2*>(sRP + 64);       // [64] alpha entering row r
+    double2* sBR = sAR + 64;                                   // [64] beta leaving row r
+    double* sLL = reinterpret_cast<double*>(sBR + 64);         // the chunk log-likelihood
+    if ((t & 15) == 15) sRP[row] = xp;   // (the same product as the suffix scan's lane 0)
     const uint32_t o0 = pk[0] & 3u;
     const double fa = model.pi[o0], fb = model.pi[o0 + 4];   // alpha_0 (b = 1 when live)
+    __syncthreads();
+    if (t < 64) {
+        // lane g < 16: rows 4g .. 4g+3 (rows past nr: identity)
+        const int g = t & 15;
+        Mat gp = mid();
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+            if (4 * g + j < nr) gp = mmul_nn(gp, sRP[4 * g + j]);
+        mnorm(gp);
+        Mat xg = gp, yg = gp;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {   // the 16 group totals: DPP scans
+            const Mat yp = row_up(xg, off), ys = row_down(yg, off);
+            xg = off < 8 ? mmul_nn(yp, xg) : mmul(yp, xg);
+            yg = off < 8 ? mmul_nn(yg, ys) : mmul(yg, ys);
+        }
+        const Mat ep = row_up(xg, 1), es = row_down(yg, 1);   // groups before / after g
+        // alpha entering group g (alpha_0 x the groups before), then its rows in order
+        double vP = fa * ep.a + fb * ep.c, vM = fa * ep.b + fb * ep.d;
+        int E = ep.e + vnorm(vP, vM);
+        double uP = es.a + es.b, uM = es.c + es.d;   // beta leaving group g (unit at the end)
+        vnorm(uP, uM);
+        double2 av[4], bv[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {   // rows 4g + j, forward
+            av[j] = make_double2(vP, vM);
+            const int r = 4 * g + j;
+            if (r < nr) {
+                const Mat R = sRP[r];
+                const double nP = vP * R.a + vM * R.c, nM = vP * R.b + vM * R.d;
+                vP = nP;
+                vM = nM;
+                E += R.e + vnorm(vP, vM);
+            }
+        }
+#pragma unroll
+        for (int j = 3; j >= 0; --j) {   // rows 4g + j, backward
+            bv[j] = make_double2(uP, uM);
+            const int r = 4 * g + j;
+            if (r < nr) {
+                const Mat R = sRP[r];
+                const double nP = R.a * uP + R.b * uM, nM = R.c * uP + R.d * uM;
+                uP = nP;
+                uM = nM;
+                vnorm(uP, uM);
+            }
+        }
+        if (t < 16) {
+#pragma unroll
+            for (int j = 0; j < 4; ++j)
+                if (4 * g + j < nr) {
+                    sAR[4 * g + j] = av[j];
+                    sBR[4 * g + j] = bv[j];
+                }
+            // the chunk log-likelihood from the last group's alpha after all rows
+            if (g == 15) *sLL = log(vP + vM) + (double)E * 0.69314718055994530942;
+        }
+    }
+    __syncthreads();
+    // every lane is past its 4-step table reads (phase 1, before the barrier above): the
+    // union becomes the bins, zeroed here, ready at the checkpoints' barrier
+    for (int i = t; i < kKeyRows * 16; i += nl) bins[i] = 0ull;
     unsigned long long* racc = acc + 2 * kSlab * (c % kAccRep);
     if (t == nl - 1) {   // the chunk log-likelihood, in signed 2^-24 units (added now: nothing
                          // stays live across the main loop)
-        const Mat A = sXP[16];
-        const double loglik =
-            log(fa * (A.a + A.b) + fb * (A.c + A.d)) + (double)A.e * 0.69314718055994530942;
-        const long long L = llrint(ldexp(loglik, kLogFix));
+        const long long L = llrint(ldexp(*sLL, kLogFix));
         acc128_add(racc + 2 * 72, (unsigned long long)L, L < 0);
     }
     double aP = fa, aM = fb;   // alpha at position p0-1 (t > 0); alpha_0 for t == 0
     if (t > 0) {
-        const Mat A = lane > 0 ? mmul(sXP[wv], up1) : sXP[wv];
-        aP = fa * A.a + fb * A.c;
-        aM = fa * A.b + fb * A.d;
+        const double2 ar = sAR[row];
+        aP = ar.x * up1.a + ar.y * up1.c;
+        aM = ar.x * up1.b + ar.y * up1.d;
     }
     vnorm(aP, aM);
-    double bP = 1.0, bM = 1.0;   // beta at the lane's last position
-    if (t + 1 < nl) {
-        const Mat B = lane < 63 ? mmul(dn1, sXS[wv]) : sXS[wv];
-        bP = B.a + B.b;
-        bM = B.c + B.d;
+    double bP, bM;   // beta at the lane's last position
+    {
+        const double2 br = sBR[row];
+        bP = dn1.a * br.x + dn1.b * br.y;
+        bM = dn1.c * br.x + dn1.d * br.y;
     }
     vnorm(bP, bM);
     // the alpha checkpoints (see 3a) of every mini-block in LDS ([m][lane], 16 B: a wave's
@@ -491,11 +522,9 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     fck[t] = make_double2(aP, aM);
     __syncthreads();
 
-    // 3a. bins (aliasing the scan buffer, read above) zeroed; alpha entering mini-block m
-    //     = alpha entering the lane times phase 1's product of the first m mini-blocks
-    //     (any per-position scale cancels in the normalised posteriors)
-    for (int i = t; i < kKeyRows * 16; i += nl) bins[i] = 0ull;
-    __syncthreads();
+    // 3a. (bins zeroed above) alpha entering mini-block m = alpha entering the lane times
+    //     phase 1's product of the first m mini-blocks (any per-position scale cancels in the
+    //     normalised posteriors)
     // 3b. mini-blocks, last to first, in TWO-POSITION BLOCKS: block j of a mini-block is its
     //     positions (2j, 2j+1), keyed by the trinucleotide tau = (x_{2j-1}, x_{2j}, x_{2j+1})
     //     and stepped by the 2-step matrix P_tau = M_{2j} M_{2j+1} (T2A/T2B).  Forward: the
@@ -533,12 +562,26 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         double alP[kB], alM[kB];
         int kf[kB / 2];   // alpha's power-of-two shifts at positions 3, 7, 11, 15 (A_2,4,6,8)
         double xP = f.x, xM = f.y;
+        // the rows are issued kFPD steps ahead (the scheduling barrier keeps them there: the
+        // compiler had waited for each step's reads right before using them, one LDS round
+        // trip on every step of the chain)
+        constexpr int kFPD = 1;   // (2: one spill at 96 VGPRs and no faster, measured)
+        double2 fa[kFPD + 1], fb[kFPD + 1];
+#pragma unroll
+        for (int j = 0; j < kFPD; ++j) {
+            fa[j] = T2A[key(j)];
+            fb[j] = T2B[key(j)];
+        }
 #pragma unroll
         for (int j = 0; j < kB; ++j) {
             alP[j] = xP;
             alM[j] = xM;
-            const uint32_t k = key(j);
-            const double2 ma = T2A[k], mb = T2B[k];
+            if (j + kFPD < kB) {
+                fa[(j + kFPD) % (kFPD + 1)] = T2A[key(j + kFPD)];
+                fb[(j + kFPD) % (kFPD + 1)] = T2B[key(j + kFPD)];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            const double2 ma = fa[j % (kFPD + 1)], mb = fb[j % (kFPD + 1)];
             const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
             xP = nP;
             xM = nM;

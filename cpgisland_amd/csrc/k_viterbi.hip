@@ -1456,12 +1456,35 @@ __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
         }
     }
     __syncthreads();
-    // B. gap composites and windows, one lane per barrier
+    // B. gap composites and windows, one lane per barrier.  The first kMaxStagedBar barriers'
+    //    plan, rx and SPLIT composites are loaded in ONE round (every load issued up front,
+    //    the composites whatever the block's type) and kept in LDS for the gaps, the anchors
+    //    and the segment entries: no further global round trip through the plans (each had
+    //    cost one memory latency on this one-workgroup-per-chunk critical path)
+    __shared__ C64 sPre[kMaxStagedBar], sPost[kMaxStagedBar];
+    __shared__ int sPt[kMaxStagedBar];
+    C64* sRx = sGap;   // rx of barrier i, replaced by its gap composite
     for (int i = t; i < nbar; i += kSegT) {
         const int k = sBar[i];
-        const VitPlan p = pl[k];
+        blc[i] = k;
+        if (i < kMaxStagedBar) {
+            const VitPlan p = pl[k];
+            const C64 r = ld_c64(rxc + k), pre = ld_c64(cp + k), post = ld_c64(cq + k);
+            int ja = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
+            int jb = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
+            if (k == 0) ja = jb = 0;   // block 0: walked by K2's head lanes
+            sWk[i] = k;
+            sWa[i] = ja;
+            sWb[i] = jb;
+            sPt[i] = p.type;
+            sRx[i] = r;
+            sPre[i] = pre;
+            sPost[i] = post;
+            continue;
+        }
+        const VitPlan p = pl[k];   // (past the staged barriers: from global memory)
         C64 R = c64_id();
-        if (i > 0) {
+        {
             const int kp = sBar[i - 1], sp = kp / kThreads, sk = k / kThreads;
             if (sp == sk) {
                 R = ld_c64(rxc + k);
@@ -1473,32 +1496,46 @@ __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
             if (pl[kp].type == PLAN_SPLIT) R = c64_mul(ld_c64(cq + kp), R);
             if (p.type == PLAN_SPLIT) R = c64_mul(R, ld_c64(cp + k));
         }
-        int ja = p.type == PLAN_SPLIT ? p.t1 : g.jfirst(k);
-        int jb = p.type == PLAN_SPLIT ? p.t2 : g.jend(k);
-        if (k == 0) ja = jb = 0;   // block 0: walked by K2's head lanes
-        blc[i] = k;
         st_c64(gpc + i, R);
-        if (i < kMaxStagedBar) {
-            sWk[i] = k;
-            sWa[i] = ja;
-            sWb[i] = jb;
-            sGap[i] = R;
-        }
     }
     __syncthreads();
+    const int nst = min(nbar, kMaxStagedBar);
+    C64 Rg = c64_id();   // the gap composite of staged barrier t
+    if (t < nst && t > 0) {
+        const int k = sWk[t], kp = sWk[t - 1], sp = kp / kThreads, sk = k / kThreads;
+        if (sp == sk) {
+            Rg = sRx[t];
+        } else {
+            Rg = sTail[sp];
+            for (int u = sp + 1; u < sk; ++u) Rg = c64_mul(Rg, sLead[u]);
+            Rg = c64_mul(Rg, sRx[t]);
+        }
+        if (sPt[t - 1] == PLAN_SPLIT) Rg = c64_mul(sPost[t - 1], Rg);
+        if (sPt[t] == PLAN_SPLIT) Rg = c64_mul(Rg, sPre[t]);
+    }
+    // the staging offsets: an exclusive scan of the window lengths (one wave; nst <= 64),
+    // overflow marked from the first window that does not fit
+    const int wlen = t < nst ? max(0, sWb[t] - sWa[t]) : 0;
+    __syncthreads();   // every lane has read its sRx before it becomes sGap
+    if (t < nst) {
+        sGap[t] = Rg;
+        st_c64(gpc + t, Rg);
+    }
+    if (t < 64) {
+        int x = wlen;
+#pragma unroll
+        for (int d = 1; d < 64; d <<= 1) {
+            const int y = __shfl_up(x, d);
+            if (t >= d) x += y;
+        }
+        const int ex = x - wlen;
+        if (t < nst) sWoff[t] = ex <= kStageSteps ? ex : kStageSteps + 1;
+        if (nst > 0 ? t == nst - 1 : t == 0)
+            sWoff[nst] = x <= kStageSteps ? x : kStageSteps + 1;
+    }
     // C. the serial chain over the barriers (k_vit_chain's phase 3)
     const uint32_t o0 = base_at(pk, 0);
     const double2 init = make_double2(vc.logpi[o0], vc.logpi[o0 + 4]);
-    const int nst = min(nbar, kMaxStagedBar);
-    if (t == 0) {
-        int o = 0;
-        for (int i = 0; i < nst; ++i) {
-            sWoff[i] = o;
-            const int len = max(0, sWb[i] - sWa[i]);
-            o = (o + len <= kStageSteps) ? o + len : kStageSteps + 1;   // overflow marker
-        }
-        sWoff[nst] = o;
-    }
     __syncthreads();
     for (int i = t >> 6; i < nst; i += kSegT / 64) {   // one wave per window
         const int off = sWoff[i];
@@ -1589,9 +1626,14 @@ __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
     }
     __syncthreads();
     // D. anchor values by block id: the barrier's exit (SPLIT: + the post composite)
-    auto anchor_val = [&](int i) {
+    auto anchor_val = [&](int i) {   // (staged barriers: plan and post composite from LDS)
+        if (i < kMaxStagedBar) {
+            double2 v = sVo[i];
+            if (sPt[i] == PLAN_SPLIT) v = c64_apply(v, sPost[i]);
+            return v;
+        }
         const int k = sBar[i];
-        double2 v = i < kMaxStagedBar ? sVo[i] : voc[i];
+        double2 v = voc[i];
         if (pl[k].type == PLAN_SPLIT) v = c64_apply(v, ld_c64(cq + k));
         return v;
     };

@@ -1,0 +1,92 @@
+"""Dev tool: build/abl/libcpg_stamp.so — the library with per-phase wall-clock stamps
+(s_memrealtime, 100 MHz) in the fused training pass, inserted into a COPY of the sources at
+anchor lines (the product sources carry no instrumentation).  Read them with
+tools/stamp_estep.py (CPG_LIB_OVERRIDE=build/abl/libcpg_stamp.so)."""
+import os
+import shutil
+import subprocess
+import sys
+
+R = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+SRC = os.path.join(R, "cpgisland_amd", "csrc")
+TREE = os.path.join(R, "build", "abl", "stamp_tree")        # csrc + include, same relative layout
+DST = os.path.join(TREE, "cpgisland_amd", "csrc")
+HEAD = '''__device__ unsigned long long g_stamp[2048 * 12];
+#define STAMP(i) do { if (threadIdx.x == 0) g_stamp[blockIdx.x * 12 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+'''
+TAIL = '''
+namespace cpg {
+extern "C" int cpg_dbg_stamps(unsigned long long* h, int n) {
+    return (int)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamp), (size_t)n * 8);
+}
+}
+'''
+K4HEAD = """__device__ unsigned long long g_stamp4[1024 * 8];
+#define STAMP4(i) do { if (threadIdx.x == 0) g_stamp4[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+"""
+K4TAIL = """
+namespace cpg {
+extern "C" int cpg_dbg_stamps4(unsigned long long* h, int n) {
+    return (int)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamp4), (size_t)n * 8);
+}
+}
+"""
+K4ANCHORS = [("    const int64_t s0 = c * nseg;", 0),
+             ("    // B. gap composites and windows, one lane per barrier.", 1),
+             ("    const int nst = min(nbar, kMaxStagedBar);\n    C64 Rg", 2),
+             ("    const bool all_staged = nst == nbar", 3),
+             ("    // D. anchor values by block id", 4),
+             ("        else ent[g.nsb] = E;\n    }\n", 5)]
+# (anchor, stamp index, before|after): the phase boundaries of k_estep_chunk
+ANCHORS = [
+    ("    const uint32_t* pk = packed + c * (C / 16);\n", 0, "after"),
+    ("    if (kCnt) {   // the lane's 64 bases", 1, "before"),
+    ("    // 4-step products: window (b0..b4)", 2, "before"),
+    ("    constexpr int L = kLanePos;            // 64 positions per lane", 3, "before"),
+    ("    // 2. ", 4, "before"),
+    ("    STAMP_ROWS", 5, "before"),
+    ("    // every lane is past its 4-step table reads", 6, "before"),
+    ("    // 3a. ", 7, "before"),
+    ("    // the epilogue's indices from an opaque copy", 9, "before"),
+    ("    // done != nullptr: the last workgroup", 10, "before"),
+]
+
+
+def main():
+    shutil.rmtree(TREE, ignore_errors=True)
+    shutil.copytree(SRC, DST)
+    shutil.copytree(os.path.join(R, "include"), os.path.join(TREE, "include"))
+    p = os.path.join(DST, "k_estep.hip")
+    s = open(p).read()
+    s = s.replace("namespace cpg {\nnamespace {\n", "namespace cpg {\nnamespace {\n" + HEAD, 1)
+    for a, i, where in ANCHORS:
+        if a == "    STAMP_ROWS":   # the barrier after the row / wave scans' shuffles
+            a = "    __syncthreads();\n    if (t < 64) {"
+        assert s.count(a) >= 1, a
+        ins = f"    STAMP({i});\n"
+        s = s.replace(a, ins + a if where == "before" else a + ins, 1)
+    s = s.replace("        reset_done(done);\n    }\n}", "        reset_done(done);\n    }\n    STAMP(11);\n}", 1)
+    s = s.replace("    STAMP(7);\n", "    STAMP(7);\n    STAMP(8);\n", 1)
+    s += TAIL
+    open(p, "w").write(s)
+    # K4 (k_vit_chain_seg): one stamp row per chunk (workgroup), thread 0
+    p = os.path.join(DST, "k_viterbi.hip")
+    s = open(p).read()
+    s = s.replace("namespace cpg {\nnamespace {\n", "namespace cpg {\nnamespace {\n" + K4HEAD, 1)
+    a = s.index("__global__ __launch_bounds__(kSegT) void k_vit_chain_seg(")
+    body = s[a:]
+    for anchor, i in K4ANCHORS:
+        assert anchor in body, anchor
+        st = f"    STAMP4({i});\n"
+        body = body.replace(anchor, anchor + st if i == 5 else st + anchor, 1)
+    s = s[:a] + body + K4TAIL
+    open(p, "w").write(s)
+    base = ("-O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function "
+            "-Wno-unused-variable --offload-arch=gfx950 -munsafe-fp-atomics " + os.environ.get("STAMP_FLAGS", ""))
+    subprocess.run(["make", "-s", "-j8", "-C", DST, "OBJDIR=../../obj",
+                    f"OUT={os.path.join(R, 'build', 'abl', 'libcpg_stamp.so')}", f"CXXFLAGS={base}", os.path.join(R, "build", "abl", "libcpg_stamp.so")],
+                   check=True)
+
+
+if __name__ == "__main__":
+    sys.exit(main())
