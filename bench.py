@@ -494,8 +494,9 @@ def main():
     ap.add_argument("--train-cus", type=int, default=-1,
                     help="run the training pass on this many compute units only (a CU-masked "
                          "stream, the first bits of the mask), leaving the rest to the decode; "
-                         "0 = all, -1 = 14/16 of them (default; with the fused decode a 400-step "
-                         "sweep read 192: 274, 208: 276, 216: 277, 224: 280, 232: 270, 240: 262)")
+                         "0 = all, -1 = 12/16 of them (default; round 3's two-position E-step, "
+                         "400 steps: 160: 295, 176: 299, 184: 302, 192: 334-348, 200: 330, "
+                         "208: 325-328, 224: 324-325, 240: 309-310 Gbase/s)")
     ap.add_argument("--decode-cus-from", type=int, default=0,
                     help="> 0: the decode stream CU-masked to compute units [this, all) (a masked "
                          "stream has no priority: the decode then runs at normal priority)")
@@ -634,7 +635,7 @@ def main():
     main_s = torch.cuda.current_stream()
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.train_cus < 0:
-        args.train_cus = ncu * 14 // 16
+        args.train_cus = ncu * 12 // 16
     if args.train_cus and args.train_cus < ncu and not args.serial:
         if args.train_cu_stride:
             tr_cus = [i for i in range(ncu) if i % args.train_cu_stride != 0][:args.train_cus]
