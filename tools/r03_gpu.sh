@@ -31,7 +31,7 @@ if [[ $STEPS == *c3* ]]; then
       --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus 2 --steps 5 --warmup 2 \
       > $OUT/c3_gloo2.json 2> $OUT/c3_gloo2.err
   rc=$?; echo "c3 gloo2 rc=$rc"; [ $rc -eq 0 ] || { tail -30 $OUT/c3_gloo2.err; exit $rc; }
-  python3 -c "import json; d=json.load(open('$OUT/c3_gloo2.json')); print('c3 gloo2', round(d['value']/1e9,1), d['ms_per_step'], d['config']['islands_found'])"
+  python3 -c "import json; d=json.loads(open('$OUT/c3_gloo2.json').read().strip().splitlines()[-1]); print('c3 gloo2', round(d['value']/1e9,1), d['ms_per_step'], d['config']['islands_found'])"
 fi
 if [[ $STEPS == *prof* ]]; then
   R=$(pwd); cd /tmp && export TMPDIR=/tmp
