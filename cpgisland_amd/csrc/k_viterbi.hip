@@ -2193,7 +2193,12 @@ __global__ __launch_bounds__(kThreads) void k_vit_fwdtrace(
     const int64_t sgi = c * nseg + sidx;
     const int64_t gid = sgi * kThreads + t;
     const int64_t k = gid - c * g.nsb;
-    // the block's 256 bases for the island tile: issued first, used after the traceback
+    __syncthreads();
+    uint4 keep[4];
+    const uint32_t org = fwd_block<true>(vc, packed, g, degen, entry, nullptr, status, rx, seg,
+                                         went, LA, LB, gid, sgi, keep);
+    // the block's 256 bases for the island tile: issued after the walk (not live across it),
+    // in flight during the look-back
     uint32_t P[16], pprev = 0u;
     {
         const uint32_t* pk = packed + c * (g.C >> 4) + k * 16;
@@ -2205,10 +2210,6 @@ __global__ __launch_bounds__(kThreads) void k_vit_fwdtrace(
         }
         if (k > 0) pprev = pk[-1];
     }
-    __syncthreads();
-    uint4 keep[4];
-    const uint32_t org = fwd_block<true>(vc, packed, g, degen, entry, nullptr, status, rx, seg,
-                                         went, LA, LB, gid, sgi, keep);
     // inclusive suffix of the segment's maps: lane l holds f_l o ... o f_255
     uint32_t x = org;
 #pragma unroll
