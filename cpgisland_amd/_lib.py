@@ -58,6 +58,8 @@ SIGNATURES = {
     "cpg_last_error": [],
     "cpg_abi_version": [],
     "cpg_reserve": [_P, _I64],
+    "cpg_reserve_ex": [_P, _I64, _INT],
+    "cpg_workspace_bytes": [_P, _P],
     "cpg_sync": [_P, _P],
     "cpg_stream_create_cu": [_INT, _P, _INT, _P],
     "cpg_stream_destroy": [_P],

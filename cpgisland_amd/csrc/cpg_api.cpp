@@ -227,18 +227,22 @@ void cpg_close(cpg_ctx* ctx) {
     delete ctx;
 }
 
-int cpg_reserve(cpg_ctx* ctx, int64_t nbases) {
-    if (!ctx || nbases < 0) return set_error(CPG_E_INVALID, "bad argument");
+int cpg_reserve(cpg_ctx* ctx, int64_t nbases) { return cpg_reserve_ex(ctx, nbases, 0); }
+
+int cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags) {
+    if (!ctx || nbases < 0 || (flags & ~CPG_RESERVE_GENERAL))
+        return set_error(CPG_E_INVALID, "bad argument");
     std::lock_guard<std::mutex> lk(ctx->mu);
     CPG_HIP(hipSetDevice(ctx->device));
     void* p;
     int rc;
-    // every slot at its largest over the chunk lengths the decode entry points take (multiples
-    // of 4096 up to the reference's 1 Mi): the per-chunk slots (look-back words, done counters)
-    // grow with the chunk count, so a reserve for 1 Mi chunks alone would still let a later call
-    // with shorter chunks grow a slot — a device-wide synchronisation (ws_get)
+    // every slot at its largest over ALL the chunk lengths the decode entry points take
+    // (every multiple of 4096 up to the reference's 1 Mi — a non-power-of-two length takes
+    // another carve): the per-chunk slots (look-back words, done counters) grow with the chunk
+    // count, so a reserve for 1 Mi chunks alone would still let a later call with shorter
+    // chunks grow a slot — a device-wide synchronisation (ws_get).  Host arithmetic only.
     size_t vit = 0, isl = 0, agg = 0, per_chunk = 0;
-    for (int64_t C = 4096; C <= CPG_DECODE_CHUNK; C *= 2) {
+    for (int64_t C = 4096; C <= CPG_DECODE_CHUNK; C += 4096) {
         const int64_t nd = nbases / C + 1;
         vit = std::max(vit, viterbi_ws_bytes(nd, C));
         isl = std::max(isl, islands_ws_bytes(nd, C));
@@ -253,6 +257,24 @@ int cpg_reserve(cpg_ctx* ctx, int64_t nbases) {
     if ((rc = ws_get(ctx, WS_IFLG, per_chunk, &p))) return rc;
     if ((rc = ws_get(ctx, WS_IDONE, per_chunk, &p))) return rc;
     if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nt, CPG_TRAIN_CHUNK), &p))) return rc;
+    if (flags & CPG_RESERVE_GENERAL) {
+        // the general path: any chunk length that is a multiple of 16 (several chunks) or the
+        // whole input as one chunk (cpg_decode_states); its ballots are sized per group of 8
+        // chunks, so the largest need is at long chunks
+        size_t gen = vitg_ws_bytes(1, std::max<int64_t>(nbases, 1));
+        for (int64_t C = 16; C <= CPG_DECODE_CHUNK && C <= nbases; C += 16)
+            gen = std::max(gen, vitg_ws_bytes(nbases / C, C));
+        if ((rc = ws_get(ctx, WS_VGEN, gen, &p))) return rc;
+    }
+    return CPG_OK;
+}
+
+int cpg_workspace_bytes(cpg_ctx* ctx, int64_t* bytes) {
+    if (!ctx || !bytes) return set_error(CPG_E_INVALID, "null argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    int64_t t = 0;
+    for (const auto& b : ctx->ws) t += (int64_t)b.bytes;
+    *bytes = t;
     return CPG_OK;
 }
 

@@ -41,7 +41,6 @@
 #include <atomic>
 #include <cfloat>
 #include <cmath>
-#include <cstdlib>
 
 #include "cpg_internal.h"
 
@@ -1690,10 +1689,7 @@ __device__ __forceinline__ uint32_t quad_origin(uint64_t hP, uint64_t hM) {
 
 // one block's re-forward (lane = block gid): backpointers, the self-check; returns the
 // block's origin map
-// kKeep (the fused forward + traceback): the four quads' words stay in registers, keep[3 - q]
-// = quad q (shifted in as they complete: static register moves), instead of going to bp.
 // sgi: the segment (workgroup of the segment path) the block belongs to.
-template <bool kKeep = false>
 __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_t* packed,
                                               const Geo& g, const uint8_t* __restrict__ degen,
                                               const double2* __restrict__ entry,
@@ -1702,22 +1698,13 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
                                               const SegSum* __restrict__ seg,
                                               const double2* __restrict__ went,
                                               const double2* LA, const double2* LB, int64_t gid,
-                                              int64_t sgi, uint4 (&keep)[4]) {
+                                              int64_t sgi) {
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     // backpointers quad-major: bp[q * nt + gid] = {bP bits 0-31, 32-63, bM bits 0-31, 32-63} of
     // the block's quad q (64 steps), so that each quad's store is one coalesced 16-B/lane row
     const int64_t nt = g.nchunks * g.nsb;
     uint4* bpo = bp + gid;
-    auto put = [&](int q, uint4 w) {
-        if constexpr (kKeep) {
-            keep[3] = keep[2];
-            keep[2] = keep[1];
-            keep[1] = keep[0];
-            keep[0] = w;
-        } else {
-            bpo[q * nt] = w;
-        }
-    };
+    auto put = [&](int q, uint4 w) { bpo[q * nt] = w; };
     if (degen[c]) {
         for (int i = 0; i < 4; ++i) put(i, make_uint4(0, 0, 0, 0));
         return 0x2u;   // identity
@@ -1973,9 +1960,8 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kK5Wav
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;   // (kScan: the grid is whole workgroups)
-    uint4 keep[4];
     const uint32_t org = fwd_block(vc, packed, g, degen, entry, bp, status, rx, seg, went, LA,
-                                   LB, gid, blockIdx.x, keep);
+                                   LB, gid, blockIdx.x);
     if constexpr (!kScan) {
         origin[gid] = (uint8_t)org;
     } else {
@@ -2160,158 +2146,6 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
     }
 }
 
-// K5 + K6 + K7 in one launch (segment path, fused islands): the workgroup walks its segment's
-// 256 blocks forward as K5 does, keeping each block's backpointer words in registers; the end
-// state of every block needs the origin maps of every LATER block of the chunk, so the
-// segments of a chunk run in reverse (workgroup b: segment nseg - 1 - b % nseg, dispatched
-// before the earlier ones) and each publishes its segment's map (aggregate) at once, then
-// looks back over the later segments' words until an inclusive one (a decoupled look-back in
-// reverse, epoch-tagged 64-bit words, bounded spin) and publishes its own inclusive map.
-// Then K7's traceback and island tile from registers: no backpointer round trip through
-// memory, one launch fewer, no per-chunk trace-scan tail.
-__global__ __launch_bounds__(kThreads) void k_vit_fwdtrace(
-    VitConsts vc, const uint32_t* packed, Geo g, const uint8_t* __restrict__ degen,
-    const double2* __restrict__ entry, uint32_t* status, const double4* __restrict__ rx,
-    const SegSum* __restrict__ seg, const double2* __restrict__ went,
-    unsigned long long* __restrict__ lbw, uint32_t epoch, double* __restrict__ score,
-    uint32_t* __restrict__ sign_out, uint32_t* zero_at, int64_t zero_n, IslFuse fz) {
-    __shared__ double2 LA[17], LB[17];
-    if (threadIdx.x < 16) {
-        LA[threadIdx.x] = make_double2(vc.L[threadIdx.x][0], vc.L[threadIdx.x][1]);
-        LB[threadIdx.x] = make_double2(vc.L[threadIdx.x][2], vc.L[threadIdx.x][3]);
-    } else if (threadIdx.x == 16) {
-        LA[16] = make_double2(0.0, -INFINITY);
-        LB[16] = make_double2(-INFINITY, 0.0);
-    }
-    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    // the undecoded tail's sign words ('-')
-    for (int64_t i = (int64_t)blockIdx.x * kThreads + t; i < zero_n; i += (int64_t)gridDim.x * kThreads)
-        zero_at[i] = 0u;
-    const int nseg = (int)(g.nsb / kThreads);
-    const int64_t c = blockIdx.x / nseg;
-    const int sidx = nseg - 1 - (int)(blockIdx.x % nseg);
-    const int64_t sgi = c * nseg + sidx;
-    const int64_t gid = sgi * kThreads + t;
-    const int64_t k = gid - c * g.nsb;
-    __syncthreads();
-    uint4 keep[4];
-    const uint32_t org = fwd_block<true>(vc, packed, g, degen, entry, nullptr, status, rx, seg,
-                                         went, LA, LB, gid, sgi, keep);
-    // the block's 256 bases for the island tile: issued after the walk (not live across it),
-    // in flight during the look-back
-    uint32_t P[16], pprev = 0u;
-    {
-        const uint32_t* pk = packed + c * (g.C >> 4) + k * 16;
-        const uint4* p4 = reinterpret_cast<const uint4*>(pk);
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const uint4 v = p4[i];
-            P[4 * i] = v.x; P[4 * i + 1] = v.y; P[4 * i + 2] = v.z; P[4 * i + 3] = v.w;
-        }
-        if (k > 0) pprev = pk[-1];
-    }
-    // inclusive suffix of the segment's maps: lane l holds f_l o ... o f_255
-    uint32_t x = org;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-        const uint32_t y = __shfl_down(x, off);
-        if (lane + off < 64) x = map_compose(x, y);
-    }
-    __shared__ uint32_t sW[kThreads / 64];
-    __shared__ uint32_t sG;   // the later segments' inclusive map
-    if (lane == 0) sW[wv] = x;
-    __syncthreads();
-    uint32_t after = 0x2u;   // the waves after this one
-    for (int w = kThreads / 64 - 1; w > wv; --w) after = map_compose(sW[w], after);
-    const uint32_t dn = __shfl_down(x, 1);
-    const uint32_t Ex = lane < 63 ? map_compose(dn, after) : after;   // f_{l+1} o ... o f_255
-    if (t == 0) {
-        uint32_t F = sW[0];
-        for (int w = 1; w < kThreads / 64; ++w) F = map_compose(F, sW[w]);
-        unsigned long long* wd = lbw + c * nseg;
-        const unsigned long long tag = (unsigned long long)epoch << 32;
-        uint32_t G = 0x2u;
-        if (sidx + 1 < nseg) {
-            __hip_atomic_store(wd + sidx, tag | F, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const unsigned long long t0 = wall_clock64();
-            for (int j = sidx + 1; j < nseg; ++j) {
-                unsigned long long f;
-                for (;;) {
-                    if (wall_clock64() - t0 >= (unsigned long long)(CPG_VIT_SPIN_LIMIT)) {
-                        atomicOr(status, ST_VIT_LOOKBACK);
-                        f = tag | 0x100u | 0x2u;
-                        break;
-                    }
-                    f = __hip_atomic_load(wd + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    if ((uint32_t)(f >> 32) == epoch) break;
-                    __builtin_amdgcn_s_sleep(1);
-                }
-                G = map_compose(G, (uint32_t)f & 0x3u);
-                if (f & 0x100u) break;   // inclusive: every later segment is in it
-            }
-        }
-        __hip_atomic_store(wd + sidx, tag | 0x100u | map_compose(F, G), __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-        sG = G;
-        if (sidx == nseg - 1 && score) {   // the chunk's final argmax (K6)
-            const double2 fin = entry[c * (g.nsb + 1) + g.nsb];
-            score[c] = (fin.y > fin.x) ? fin.y : fin.x;
-        }
-    }
-    __syncthreads();
-    const double2 fin = entry[c * (g.nsb + 1) + g.nsb];
-    const uint32_t s_end = (fin.y > fin.x) ? 0u : 1u;   // '+' first: '-' only if strictly >
-    uint32_t s = map_apply(map_compose(Ex, sG), s_end);   // state at the block's last position
-    const uint32_t sb_exp = map_apply(org, s);             // the state before the block
-    // K7's word-parallel traceback from the registers (words: keep[3 - q] = quad q)
-    uint32_t wP[8], wM[8];
-    wP[0] = keep[3].x; wP[1] = keep[3].y; wM[0] = keep[3].z; wM[1] = keep[3].w;
-    wP[2] = keep[2].x; wP[3] = keep[2].y; wM[2] = keep[2].z; wM[3] = keep[2].w;
-    wP[4] = keep[1].x; wP[5] = keep[1].y; wM[4] = keep[1].z; wM[5] = keep[1].w;
-    wP[6] = keep[0].x; wP[7] = keep[0].y; wM[6] = keep[0].z; wM[7] = keep[0].w;
-    const int jend = g.jend(k);
-    uint32_t out[8];
-#pragma unroll
-    for (int w = 7; w >= 0; --w) {
-        const int n = jend - 32 * w;
-        const uint32_t vm = n >= 32 ? 0xFFFFFFFFu : (n <= 0 ? 0u : (1u << n) - 1u);
-        const uint32_t A = ~wP[w] | ~vm, B = ~wM[w] & vm;
-        uint32_t X = (A >> 1) | 0x80000000u, Y = B >> 1;
-#pragma unroll
-        for (int d = 1; d < 32; d <<= 1) {
-            const uint32_t Xg = __builtin_amdgcn_alignbit(0xFFFFFFFFu, X, d);
-            const uint32_t Yg = Y >> d;
-            const uint32_t nX = (Xg & X) | (~Xg & Y), nY = (Yg & X) | (~Yg & Y);
-            X = nX;
-            Y = nY;
-        }
-        const uint32_t S = s ? X : Y;
-        out[w] = S & vm;
-        s = (S & 1u) ? (A & 1u) : (B & 1u);
-    }
-    const uint32_t sb = k > 0 ? sb_exp : 0u;
-    if (k > 0 && s != sb) atomicOr(status, ST_VERIFY_CHAIN);
-    uint32_t* so = sign_out + c * (g.C >> 5) + k * 8;
-    uint4* s4 = reinterpret_cast<uint4*>(so);   // (whole blocks: chunk_len == nsb * 256)
-    s4[0] = make_uint4(out[0], out[1], out[2], out[3]);
-    s4[1] = make_uint4(out[4], out[5], out[6], out[7]);
-    trace_tile(out, P, pprev, sb << 31, k, fz.ws, sgi);
-    __shared__ int s_last;
-    __builtin_amdgcn_s_waitcnt(0);   // this wave's record stores have completed
-    __syncthreads();
-    if (t == 0) {
-        const unsigned old = __hip_atomic_fetch_add(fz.done + c, 1u, __ATOMIC_RELAXED,
-                                                    __HIP_MEMORY_SCOPE_AGENT);
-        s_last = old == (unsigned)nseg - 1;
-        if (s_last) __hip_atomic_store(fz.done + c, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    __syncthreads();
-    if (!s_last) return;
-    __shared__ isl::ResolveLds L;
-    __shared__ isl::Cnt5 s_to[kThreads / 16];
-    isl::resolve_chunk<true, kThreads / 16>(packed, g.C, fz.ws, fz.o, c, L, s_to);
-}
-
 // ---------------------------------------------------------------- workspace layout
 struct VitWs {
     int4* comp1;
@@ -2374,9 +2208,9 @@ VitWs carve(void* base, int64_t nchunks, int64_t nsb) {
 
 int64_t vit_nsb(int64_t chunk_len) { return chunk_len <= 1 ? 1 : (chunk_len + kSB - 1) / kSB; }
 
-// [segment][8] K1's segment products, then [segment] the fused trace's suffix maps
+// [segment][8] K1's segment products
 size_t viterbi_agg_bytes(int64_t nchunks, int64_t chunk_len) {
-    return (size_t)(nchunks * vit_nsb(chunk_len) / kThreads + 1) * 9 * sizeof(unsigned long long);
+    return (size_t)(nchunks * vit_nsb(chunk_len) / kThreads + 1) * 8 * sizeof(unsigned long long);
 }
 
 size_t viterbi_ws_bytes(int64_t nchunks, int64_t chunk_len) {
@@ -2432,20 +2266,6 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
         hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kChainT), 0, s, vc, packed,
                            g, w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout,
                            w.vhead);
-    // segment path with the fused island scan: forward, trace scan and traceback in one launch
-    static const bool fuse57 = std::getenv("CPG_VIT_FUSE57") != nullptr;
-    if (segp && fuse && done5 && fuse57) {
-        if (fuse->ws.ntile != nsb / kThreads) return hipErrorInvalidValue;
-        unsigned long long* lbw = agg + (nt / kThreads + 1) * 8;
-        hipLaunchKernelGGL(k_vit_fwdtrace, dim3(grid), dim3(kThreads), 0, s, vc, packed, g,
-                           w.degen, w.entry, status, w.gk, sg, w.went, lbw, as.epoch, score,
-                           sign_out, zero_at, zero_n, *fuse);
-        if (degen_out) {
-            hipError_t e = hipMemcpyAsync(degen_out, w.degen, nchunks, hipMemcpyDeviceToDevice, s);
-            if (e != hipSuccess) return e;
-        }
-        return hipGetLastError();
-    }
     // chunks of whole K5 workgroups: the trace scan runs in each chunk's last K5 workgroup
     if (done5 && nsb % kThreads == 0) {
         hipLaunchKernelGGL(k_vit_forward<true>, dim3(grid), dim3(kThreads), 0, s, vc, packed, g,

@@ -95,8 +95,16 @@ class Context:
     def sync(self, stream=None):
         check(lib.cpg_sync(self.handle, stream))
 
-    def reserve(self, nbases: int):
-        check(lib.cpg_reserve(self.handle, int(nbases)))
+    def reserve(self, nbases: int, general: bool = False):
+        """cpg_reserve / cpg_reserve_ex: size the workspace for inputs of up to nbases bases
+        (general=True: also the general-model Viterbi's, ~26 B per base)."""
+        check(lib.cpg_reserve_ex(self.handle, int(nbases), 1 if general else 0))
+
+    def workspace_bytes(self) -> int:
+        """cpg_workspace_bytes: device workspace held by the context."""
+        v = C.c_int64()
+        check(lib.cpg_workspace_bytes(self.handle, C.byref(v)))
+        return v.value
 
 
 _default_ctx: Context | None = None

@@ -106,11 +106,20 @@ void        cpg_close(cpg_ctx* ctx);
 const char* cpg_last_error(void);
 int         cpg_abi_version(void);
 /* Pre-size the context's workspace for inputs of up to nbases bases, for every chunk length
- * the entry points take (multiples of 4096 up to 1 Mi), so that the _d entry points never
- * allocate (required before hipGraph capture).  A slot that has to grow later (a larger
- * input) synchronises the whole device first: the old buffer may still be read by a kernel
- * on another stream. */
+ * the exact-scan entry points take (every multiple of 4096 up to 1 Mi), so that the _d entry
+ * points never allocate (required before hipGraph capture).  A slot that has to grow later (a
+ * larger input) synchronises the whole device first: the old buffer may still be read by a
+ * kernel on another stream.
+ * The general-model Viterbi (cpg_viterbi_states_d, and cpg_viterbi_d / cpg_decode_d /
+ * cpg_decode_states for models outside the exact scan's contract) needs up to ~26 B of
+ * workspace per base (its backpointer ballots); cpg_reserve does NOT size it: that path
+ * allocates at its first use and is outside this contract unless the workspace was reserved
+ * with cpg_reserve_ex(ctx, nbases, CPG_RESERVE_GENERAL). */
 int         cpg_reserve(cpg_ctx* ctx, int64_t nbases);
+#define CPG_RESERVE_GENERAL 1   /* also size the general-model Viterbi's workspace */
+int         cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags);
+/* Device workspace currently held by the context, in bytes (all slots). */
+int         cpg_workspace_bytes(cpg_ctx* ctx, int64_t* bytes);
 /* Wait for `stream` and return the first kernel-reported status since the last
  * cpg_sync: CPG_OK; CPG_E_VERIFY (a Viterbi exactness self-check failed); CPG_E_INVALID
  * (a broken contig layout); CPG_E_DEVICE when a bounded look-back gave up — the island
@@ -217,7 +226,11 @@ int cpg_merge_train_d(cpg_ctx* ctx, const void* d_gathered, int world, double* d
  * cpg_sync reports CPG_E_UNSUPPORTED if their path leaves the bases' states (a dead end of
  * zero transitions: sign bits cannot carry it); non-deterministic emission rows:
  * CPG_E_UNSUPPORTED at once (use cpg_viterbi_states_d or cpg_decode_d).  chunk_len: a
- * multiple of 256 when there is more than one chunk. */
+ * multiple of 256 when there is more than one chunk.
+ * A chunk with pi = 0 for both live states of its first base ("degenerate") decodes, as in
+ * Mahout's loop, to the all-state-0 path with score -inf: its sign bits (all
+ * '+') do not represent that path — a -inf d_score marks such chunks (cpg_viterbi_states_d
+ * returns the states themselves). */
 int cpg_viterbi_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                   int64_t nbases, int64_t chunk_len, uint32_t* d_sign_out,
                   double* d_score, void* stream);

@@ -148,3 +148,38 @@ def test_decode_d_non_deterministic_emissions(gpu_ctx, dev):
     ref_isl["beg1"] += 5 * C
     ref_isl["end1"] += 5 * C
     assert len(ref_isl) > 0 and np.array_equal(isl, ref_isl)
+
+
+def test_reserved_general_path_does_not_allocate(dev):
+    """ cpg_reserve_ex(CPG_RESERVE_GENERAL) sizes the general-model Viterbi's
+    workspace: after it, decodes that take the general path (zero transitions, several chunk
+    lengths, the whole input as one chunk) and the exact-scan path (a non-power-of-two chunk
+    length) leave the context's workspace unchanged — no allocation, no device-wide sync, so
+    the calls are safe to capture in a hipGraph.  Results still equal the oracle's."""
+    import torch
+    from cpgisland_amd import Context, HmmModel
+    from cpgisland_amd import device as D
+    rng = np.random.default_rng(5)
+    pi, a, b = co.model_split(co.initial_model())
+    a2 = a.copy()
+    a2[0, 5] = 0.0
+    a2 /= a2.sum(1, keepdims=True)
+    mg = co.model_flat(pi, a2, b)
+    n = 5 * 65536 + 333
+    obs = rng.integers(0, 4, n).astype(np.uint8)
+    dp = _dev(pr.pack(obs), dev)
+    ctx = Context(0)
+    try:
+        ctx.reserve(n, general=True)
+        before = ctx.workspace_bytes()
+        for C in (4096, 65536, 12288):
+            D.viterbi(ctx, HmmModel.from_struct(mg), dp, n, C)
+            D.viterbi(ctx, HmmModel.initial(), dp, n, C)
+        st, sc = D.viterbi_states(ctx, HmmModel.from_struct(mg), dp, n, n)   # one chunk
+        torch.cuda.synchronize()
+        ctx.sync()
+        assert ctx.workspace_bytes() == before
+        ref, best = co.viterbi8(mg, obs)
+        assert np.array_equal(st.cpu().numpy()[:n], ref) and sc.cpu().numpy()[0] == best
+    finally:
+        ctx.close()
