@@ -41,29 +41,67 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # (the second forward pass over half of each mini-block) not counted
 FP64_PEAK_TFLOPS = 78.6
 ESTEP_FLOPS_PER_BASE = 23
-# algorithmic bytes per base of each phase
-BYTES_PER_BASE = {"estep": 0.25, "counts": 0.375, "viterbi": 0.375, "islands": 0.375}
+# algorithmic bytes per base of each phase: the fused
+# decode (cpg_decode_d) reads the packed bases once and writes the 1-bit path (0.375); the
+# separate island call re-reads bases + path (another 0.375)
+BYTES_PER_BASE = {"estep": 0.25, "counts": 0.375, "viterbi": 0.375, "islands": 0.375,
+                  "decode_fused": 0.375}
+# VALU issue roof: one wave64 instruction per 2 cycles per SIMD (SIMD-32, MI355X_MICROARCH.md
+# "Wave scheduling"), 1,024 SIMDs at 2.4 GHz; fp64 instructions occupy the SIMD twice as long,
+# so for an fp64-heavy mix the true roof is lower — the fraction is an upper bound on issue use
+VALU_PEAK_WINST = 1024 * 2.4e9 / 2
+DECODE_KERNELS = ("k_vit_approx", "k_vit_scan", "k_vit_exact", "k_vit_chain", "k_vit_chain_seg",
+                  "k_vit_forward", "k_vit_tscan", "k_vit_trace", "k_isl_tile", "k_isl_resolve")
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def _pmc_traffic(kernel, nbases):
-    """HBM bytes per launch of `kernel` from the committed PMC summary of this bench
-    (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction of
-    MI355X_MICROARCH.md), when it was collected on the same workload size."""
-    path = os.path.join(ROOT, "profiles", "pmc_latest.json")
+def _pmc(name):
     try:
-        with open(path) as f:
-            d = json.load(f)
-        k = d["kernels"][kernel]
-        if d.get("bases") != nbases:
-            return None
-        return {"traffic_bytes": int(k["traffic_bytes"]),
-                "source": f"profiles/pmc_latest.json ({d.get('collected', '?')})"}
-    except (OSError, KeyError, ValueError):
+        with open(os.path.join(ROOT, "profiles", name)) as f:
+            return json.load(f)
+    except (OSError, ValueError):
         return None
+
+
+def _pmc_traffic(kernel, nbases, name="pmc_latest.json", scale=False):
+    """HBM bytes per launch of `kernel` from a committed PMC summary of this bench
+    (tools/pmc.sh + tools/pmc_summary.py: FETCH_SIZE x2 + WRITE_SIZE, gfx950 correction of
+    MI355X_MICROARCH.md): as collected when it was collected on the same workload size, or
+    (scale=True: the N>1 shards) scaled linearly from the bytes per base of that profile."""
+    d = _pmc(name)
+    try:
+        k = d["kernels"][kernel]
+        b = d.get("bases")
+        if b != nbases and not (scale and b):
+            return None
+        t = k["traffic_bytes"] if b == nbases else k["traffic_bytes"] / b * nbases
+        return {"traffic_bytes": int(t),
+                "source": f"profiles/{name} ({d.get('collected', '?')})" +
+                          ("" if b == nbases else f", scaled from {b} bases")}
+    except (TypeError, KeyError, ValueError):
+        return None
+
+
+def _decode_valu(nbases, phase_ms, name="pmc_latest.json"):
+    """VALU issue roofline of the decode phase: wave-level VALU instructions per call of its
+    kernels (PMC SQ_INSTS_VALU, committed profile of the same size) / the phase time, against
+    VALU_PEAK_WINST."""
+    d = _pmc(name)
+    if not d or d.get("bases") != nbases or phase_ms <= 0:
+        return None
+    ks = {k: v for k, v in d["kernels"].items() if k in DECODE_KERNELS and "SQ_INSTS_VALU" in v}
+    if not ks:
+        return None
+    winst = sum(v["SQ_INSTS_VALU"] for v in ks.values())
+    ach = winst / (phase_ms / 1e3)
+    return {"bound": "valu-issue", "phase": "decode", "kernels": sorted(ks),
+            "valu_wave_instructions": int(winst), "achieved": round(ach / 1e9, 2),
+            "peak": round(VALU_PEAK_WINST / 1e9, 1), "unit": "G wave-instructions/s",
+            "frac": round(ach / VALU_PEAK_WINST, 4),
+            "source": f"profiles/{name} ({d.get('collected', '?')})"}
 
 
 def cpu_baseline(seed, sample_bases, threads):
@@ -242,7 +280,43 @@ def _gather0(t, world, rank, backend, out_list):
             o.copy_(x)
 
 
-def run_c3(args, world, rank, local, dist, backend, dev):
+def count_leg(ctx, dp, ds, n, reps=20):
+    """The labelled-count kernel (cpg_count_labelled_d) alone over an
+    HBM-resident genome (the C3 genome: 1.16 GB of packed bases + label bits, far past the
+    256 MB Infinity Cache): HIP events around each call on the stream it runs on; the
+    north_star's count-kernel roofline."""
+    from cpgisland_amd import device as D
+    out = torch.empty(124, dtype=torch.int64, device=dp.device)
+    for _ in range(3):
+        D.count_labelled(ctx, dp, ds, n, TRAIN, out=out)
+    ev = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        D.count_labelled(ctx, dp, ds, n, TRAIN, out=out)
+        b.record()
+        ev.append((a, b))
+    torch.cuda.synchronize()
+    ctx.sync(None)
+    ms = sorted(a.elapsed_time(b) for a, b in ev)[reps // 2]
+    c = out.cpu().numpy()
+    nch = n // TRAIN
+    ok = bool(c[:8].sum() == nch and c[8:72].sum() == nch * (TRAIN - 1) and c[120:].sum() == n)
+    bpb = BYTES_PER_BASE["counts"]
+    ach = bpb * n / (ms / 1e3) / 1e9
+    r = {"bound": "hbm", "kernel": "k_count_main", "bases": n, "achieved": round(ach, 1),
+         "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(ach / HBM_PEAK_GBS, 4),
+         "traffic": None, "algorithmic_bytes": bpb * n, "bytes_per_base": bpb,
+         "ms_median": round(ms, 4), "reps": reps, "identities_ok": ok,
+         "note": "median of event-timed calls over the HBM-resident C3 genome"}
+    pmc = _pmc_traffic("k_count_main", n, name="pmc_count.json")
+    if pmc:
+        r["traffic"] = pmc["traffic_bytes"]
+        r["traffic_source"] = "stored PMC profile, not this run: " + pmc["source"]
+    return r
+
+
+def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
     """configs[2] — the north_star workload: ONE 3.1 Gbp genome split evenly over the world's
     ranks at multiples of 64 bases (cpgisland_amd/dist.py shard_bounds(align=64), not at chunk
     boundaries).  A chunk belongs to the rank holding its first base; a rank's last chunk is
@@ -309,9 +383,13 @@ def run_c3(args, world, rank, local, dist, backend, dev):
     gat_c = [[torch.empty(1, dtype=torch.int64, device=dev) for _ in range(world)]
              if rank == 0 else None for _ in range(2)]
     main_s = torch.cuda.current_stream()
-    s_halo, s_tr, s_dec, s_red, s_isl = (torch.cuda.Stream(), torch.cuda.Stream(),
-                                         torch.cuda.Stream(priority=-1), torch.cuda.Stream(),
-                                         torch.cuda.Stream())
+    ncu = torch.cuda.get_device_properties(dev).multi_processor_count
+    ntc = args.c3_train_cus if 0 < args.c3_train_cus < ncu else 0
+    # the training pass on a CU-masked stream of ntc compute units (0: every CU), the decode
+    # at high priority on all of them
+    s_tr = D.cu_stream(local, list(range(ntc))) if ntc else torch.cuda.Stream()
+    s_halo, s_dec, s_red, s_isl = (torch.cuda.Stream(), torch.cuda.Stream(priority=-1 if args.prio else 0),
+                                   torch.cuda.Stream(), torch.cuda.Stream())
     ev = {k: [torch.cuda.Event() for _ in range(2)] for k in
           ("halo", "tr_done", "dec_done", "rec", "red", "isl")}
     ntr = []   # (start, end) timing events of the training pass, every 4th timed step
@@ -426,6 +504,8 @@ def run_c3(args, world, rank, local, dist, backend, dev):
                           "decode_chunks": nd_total, "island_capacity_per_rank": icap,
                           "collectives": (("rccl" if backend == "nccl" else backend)
                                           if dist else None),
+                          "train_cus": ntc or ncu,
+                          "decode_priority": "high" if args.prio else "normal",
                           "islands_found": sum(counts)},
                "phases_ms": {"train_pass": round(tr_ms, 4)},
                "host_issue_ms_per_step": round(issue * 1e3 / args.steps, 4),
@@ -433,11 +513,29 @@ def run_c3(args, world, rank, local, dist, backend, dev):
                             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                             "algorithmic_bytes": bpb * tr_n, "bytes_per_base": bpb},
-               "cpu_baseline": None}
-        print(json.dumps(out), flush=True)
+               "cpu_baseline": None,
+               "cpu_baseline_note": ("the CPU baseline is measured on rank 0 at N = 1 only (the "
+                                     "bench contract): the n_gpus = 1 line's cpu_baseline, the "
+                                     "oracle on a bounded sample of the same synthetic genome")}
+        # HBM traffic of the training pass at this rank's size: the PMC profile of the C3
+        # workload on one GPU (tools/pmc.sh c3), scaled to the shard's bases
+        pmc = _pmc_traffic("k_estep_chunk", tr_n, name="pmc_c3.json", scale=True)
+        if pmc:
+            out["roofline"]["traffic"] = pmc["traffic_bytes"]
+            out["roofline"]["traffic_source"] = "stored PMC profile, not this run: " + pmc["source"]
+        if world == 1:   # the count kernel alone over the same HBM-resident genome
+            out["roofline_count"] = count_leg(ctx, bufs[0][0][tr_o // 16:], bufs[0][1][tr_o // 32:],
+                                              tr_n)
+        if emit:
+            print(json.dumps(out), flush=True)
+    else:
+        out = None
+    if ntc:
+        D.cu_stream_destroy(s_tr)
     ctx.close()
     if dist:
         torch.distributed.destroy_process_group()
+    return out
 
 
 def main():
@@ -458,6 +556,13 @@ def main():
                          "split over the GPUs (configs[2], the north_star workload, strong "
                          "scaling); auto: c2 on one GPU, c3 on several")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--c3-train-cus", type=int, default=0,
+                    help="C3 workload: the training pass on a CU-masked stream of this many compute "
+                         "units (0 = all; the decode stream runs on all of them at high priority)")
+    ap.add_argument("--c3-steps", type=int, default=20,
+                    help="N=1: timed steps of the C3 leg (the 3.1 Gbp strong-scaling workload of "
+                         "the N>1 lines on this one GPU, reported as c3_single_gpu, with the "
+                         "count kernel's HBM roofline over its genome); 0 = skip")
     ap.add_argument("--probe-sleep", type=str, default="",
                     help="measurement probe: STREAM:CYCLES adds a one-thread spin kernel "
                          "(torch.cuda._sleep) per step on the decode ('dec') or training ('tr') "
@@ -850,6 +955,19 @@ def main():
     if args.cold_steps > 0 and not dist and not args.flush_mb:
         cold = cold_cache_steps(lanes[0], dp, ds, N, model0, model1, args.cold_steps, main_s, dev,
                                 fused=fused, fused_decode=fused_decode)
+    # N = 1: the C3 strong-scaling workload (the one the N > 1 lines run) on this one GPU, a
+    # short leg after the headline, plus the count kernel over its HBM-resident genome
+    c3_leg = None
+    if not dist and args.c3_steps > 0:
+        import copy
+        a3 = copy.copy(args)
+        a3.steps, a3.warmup, a3.bases = args.c3_steps, 3, C3_BASES
+        c3_leg = run_c3(a3, 1, 0, local, False, backend, dev, emit=False)
+        if c3_leg is not None:
+            c3_leg = {k: c3_leg[k] for k in ("value", "unit", "ms_per_step", "steps",
+                                              "warmup_steps_run", "scaling", "config",
+                                              "phases_ms", "roofline", "roofline_count")
+                      if k in c3_leg}
     steps = args.steps
     ms_per_step = elapsed * 1e3 / steps
     value = N * world * steps / elapsed
@@ -891,11 +1009,14 @@ def main():
                      "frac": round(fl / FP64_PEAK_TFLOPS, 4),
                      "flops_per_base": ESTEP_FLOPS_PER_BASE}
         vit = phases["decode"] if "decode" in phases else phases["viterbi"] + phases["islands"]
-        roof_decode = {"phase": "viterbi+islands", "achieved": round(
-            (BYTES_PER_BASE["viterbi"] + BYTES_PER_BASE["islands"]) * N / (vit / 1e3) / 1e9
-            if vit > 0 else 0.0, 1),
-            "unit": "GB/s", "frac": None}
+        dbpb = (BYTES_PER_BASE["decode_fused"] if fused_decode else
+                BYTES_PER_BASE["viterbi"] + BYTES_PER_BASE["islands"])
+        roof_decode = {"bound": "hbm", "phase": "viterbi+islands", "achieved": round(
+            dbpb * N / (vit / 1e3) / 1e9 if vit > 0 else 0.0, 1),
+            "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": None, "bytes_per_base": dbpb,
+            "algorithmic_bytes": dbpb * N}
         roof_decode["frac"] = round(roof_decode["achieved"] / HBM_PEAK_GBS, 4)
+        roof_decode_valu = _decode_valu(N, vit)
         out = {"metric": METRIC, "value": value, "unit": "bases/s", "n_gpus": world,
                "steps": steps, "warmup": args.warmup, "warmup_steps_run": nwarm,
                "settle_ms": args.settle_ms, "ms_per_step": ms_per_step,
@@ -934,12 +1055,15 @@ def main():
                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
                "host_issue_ms_per_step": round(issue * 1e3 / steps, 4),
                "roofline": roof, "roofline_fp64": roof_fp64, "roofline_decode": roof_decode,
-               "cold_cache": cold}
+               "roofline_decode_valu": roof_decode_valu, "cold_cache": cold}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(SEED, args.cpu_sample,
                                                 min(args.cpu_threads, os.cpu_count() or 1))
         else:
             out["cpu_baseline"] = None
+        out["c3_single_gpu"] = c3_leg
+        if c3_leg is not None:
+            out["roofline_count"] = c3_leg.pop("roofline_count", None)
         print(json.dumps(out), flush=True)
     for ln in lanes:
         for cx3, st in ln["tr"]:

@@ -17,18 +17,8 @@ constexpr int kRaw = 72;        // tot[16] pp[16] pm[16] mp[16] init[8]
 constexpr int kRep = 16;        // replicated accumulator sets (workgroup b adds into b % kRep)
 constexpr uint32_t M55 = 0x55555555u;
 
-struct Masks {
-    uint32_t e[4];   // bit 2k set iff base k == b
-};
-__device__ __forceinline__ Masks base_masks(uint32_t w) {
-    const uint32_t h = w >> 1;
-    Masks m;
-    m.e[0] = ~(w | h) & M55;
-    m.e[1] = w & ~h & M55;
-    m.e[2] = h & ~w & M55;
-    m.e[3] = w & h & M55;
-    return m;
-}
+// (m & x) | (~m & y): one v_bfi_b32
+__device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) { return (m & x) | (~m & y); }
 // 16 bits (bit k) -> even bit positions (bit 2k)
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {
     x &= 0xFFFFu;
@@ -49,103 +39,136 @@ __device__ __forceinline__ uint32_t compact16(uint32_t x) {
     return x;
 }
 
-// One lane's register counters.  The 16 dinucleotide counts of a set of transitions are
-// kept in a BASIS of 16 sums from which they follow exactly (class_of): the 9 counts with
-// p, b < 3 (p the previous base), the 3 row sums (previous base p < 3), the 3 column sums
-// (base b < 3) and the number of transitions — 9 AND+popcounts and 6 popcounts per word pair
-// instead of 16 ANDs + 16 popcounts per word, and masks for three base values, not four.
-// Two words are counted at once: a word's base masks sit on the even bits, the next word's
-// are shifted onto the odd bits of the same register (popcounts do not care about order).
-// Two 16-bit fields per basis sum: all transitions (low half) and the '+'->'+' ones (high
-// half); a block without a '+' state skips the sign work.  Sign changes (island borders: a
-// few per island) go to the LDS counters lds[32 .. 64) one by one.  A field grows by at most
-// 64 per block and flush() sums 64 lanes, so a lane flushes at least every 15 blocks.
+// One lane's register counters.  The 16 dinucleotide counts of a set of transitions are kept
+// as their 16 MOMENTS: with the four bit-planes of a transition — lo / hi bit of the current
+// base b and lo / hi bit of the previous base p — moment S (S = a subset of the planes, bit 0
+// lo, bit 1 hi, bit 2 previous lo, bit 3 previous hi) counts the transitions whose planes in S
+// are all 1, moment 0 the transitions themselves.  The count of dinucleotide d = p * 4 + b
+// follows by Moebius inversion, N(d) = sum over S containing d of (-1)^|S \ d| m_S (raw_of):
+// 11 ANDs + 15 v_bcnt per 32 positions on four planes, which cost 11 instructions to form
+// (two words at once: a word's positions on the even bits, the next word's on the odd bits
+// of the same register — popcounts do not care about order).  The registers hold the moments
+// of ALL transitions (32-bit: flushed once per kernel or per caller's batch); the moments of
+// the '+'->'+' transitions and the sign changes (island borders: a few per island) occur in
+// few blocks and go to the LDS counters at once (lds[16 .. 32) and lds[32 .. 64)), so the
+// common block — no '+' state — adds each popcount straight into its register.
 struct Lane {
-    static constexpr int kMaxBlocks = 15;
     uint32_t c[16];
-    __device__ __forceinline__ Lane() {
+    // pprep != nullptr: the '+'->'+' moments go to 16 x 16 lane-spread LDS replicas
+    // (pprep[moment * 16 + lane % 16]; the caller sums them: pp_replicas_sum) by the lanes
+    // that have '+' states; nullptr: the whole wave runs the '+' work when one lane needs it
+    // and adds one wave sum per moment to lds[16 .. 32)
+    uint32_t* pprep;
+    __device__ __forceinline__ explicit Lane(uint32_t* pp_replicas = nullptr) : pprep(pp_replicas) {
 #pragma unroll
         for (int d = 0; d < 16; ++d) c[d] = 0u;
     }
-    struct M3 {
-        uint32_t e[3];   // bit 2k set iff base k == b (b < 3)
-    };
-    static __device__ __forceinline__ M3 masks3(uint32_t w) {
-        const uint32_t h = w >> 1;
-        return M3{{~(w | h) & M55, w & ~h & M55, h & ~w & M55}};
-    }
     // w: the block's 4 packed words; s: its 2 sign words; wprev / sprev: the packed word and
-    // the sign bit before the block (ignored at a chunk start: no transition into position 0).
-    // Two code paths chosen per lane (a wave runs the '+' path only if one of its lanes needs
-    // it): as selects, the compiler computed the '+' path's 16-bit high fields always.
+    // the sign bit before the block (ignored at a chunk start: no transition into position 0);
+    // valid = false: a lane without a block (counts nothing).  EVERY lane of the wave calls
+    // (the '+' work below reduces over the wave).
     __device__ __forceinline__ void block(uint4 w, uint2 s, uint32_t wprev, uint32_t sprev,
-                                          bool cstart, uint32_t* lds) {
+                                          bool cstart, uint32_t* lds, bool valid = true) {
         if (cstart) sprev = 0u;
-        if ((s.x | s.y | sprev) != 0u) block_t<true>(w, s, wprev, sprev, cstart, lds);
-        else block_t<false>(w, s, wprev, sprev, cstart, lds);
-    }
-    template <bool kPlus>
-    __device__ __forceinline__ void block_t(uint4 w, uint2 s, uint32_t wprev, uint32_t sprev,
-                                            bool cstart, uint32_t* lds) {
+        const uint32_t vm = valid ? ~0u : 0u;
         const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-        const uint32_t sw[4] = {s.x & 0xFFFFu, s.x >> 16, s.y & 0xFFFFu, s.y >> 16};
-        M3 last = masks3(wprev);
-        uint32_t sprv = sprev & 1u;
-        uint64_t ch = 0u;   // positions whose sign differs from the previous position's
+        uint32_t last = wprev;
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
-            const M3 ea = masks3(ww[2 * pr]), eb = masks3(ww[2 * pr + 1]);
-            uint32_t P[3], E[3], Ec[3];
+            const uint32_t a = ww[2 * pr], b = ww[2 * pr + 1];
+            // planes of the 32 positions: word a's position k at bit 2k, word b's at 2k+1
+            uint32_t LO = bfi(M55, a, b << 1);
+            uint32_t HI = bfi(M55, a >> 1, b);
+            // the previous base's planes: position k-1 of the same word two bits below; bit 0
+            // (a[0]) from the word before a (its position 15: bits 30 / 31), bit 1 (b[0]) from
+            // a[15] (bit 30 of the planes) — through bits 30 / 31 of an aligned pair
+            uint32_t PLO = __builtin_amdgcn_alignbit(LO, bfi(0x80000000u, LO << 1, last), 30);
+            uint32_t PHI = __builtin_amdgcn_alignbit(HI, bfi(0x80000000u, HI << 1, last >> 1), 30);
+            // no transition into a chunk's position 0, nothing from a lane without a block
+            const uint32_t pm = (pr == 0 && cstart) ? (vm & ~1u) : vm;
+            LO &= pm; HI &= pm; PLO &= pm; PHI &= pm;
+            last = b;
+            const uint32_t lh = LO & HI, pq = PLO & PHI;
+            const uint32_t x[16] = {0u, LO, HI, lh, PLO, LO & PLO, HI & PLO, lh & PLO,
+                                    PHI, LO & PHI, HI & PHI, lh & PHI, pq, LO & pq, HI & pq, lh & pq};
 #pragma unroll
-            for (int b = 0; b < 3; ++b) {
-                uint32_t pa = __builtin_amdgcn_alignbit(ea.e[b], last.e[b], 30);
-                if (pr == 0 && cstart) pa &= ~1u;   // no transition into position 0
-                const uint32_t pb = __builtin_amdgcn_alignbit(eb.e[b], ea.e[b], 30);
-                P[b] = pa | (pb << 1);
-                E[b] = ea.e[b] | (eb.e[b] << 1);
-                Ec[b] = (pr == 0 && cstart) ? (E[b] & ~1u) : E[b];   // column: positions with a transition
-            }
-            last = eb;
-            uint32_t PP = 0u;
-            if (kPlus) {
-                uint32_t pp2[2];
-#pragma unroll
-                for (int h = 0; h < 2; ++h) {
-                    const int k = 2 * pr + h;
-                    const uint32_t S = spread16(sw[k]);
-                    const uint32_t Sp = (S << 2) | sprv;   // sign of the previous position
-                    sprv = sw[k] >> 15;
-                    pp2[h] = Sp & S;   // bit 0 of a chunk's first word: Sp = 0
-                    uint32_t chg = (Sp ^ S) & M55;
-                    if (k == 0 && cstart) chg &= ~1u;
-                    ch |= (uint64_t)compact16(chg) << (16 * k);
-                }
-                PP = pp2[0] | (pp2[1] << 1);
-            }
-            auto add = [&](int j, uint32_t x) {
-                c[j] += kPlus ? __popc(x) + (__popc(x & PP) << 16) : __popc(x);
-            };
-#pragma unroll
-            for (int p = 0; p < 3; ++p)
-#pragma unroll
-                for (int b = 0; b < 3; ++b) add(p * 3 + b, P[p] & E[b]);
-#pragma unroll
-            for (int p = 0; p < 3; ++p) add(9 + p, P[p]);
-#pragma unroll
-            for (int b = 0; b < 3; ++b) add(12 + b, Ec[b]);
-            if (kPlus) c[15] += __popc(PP) << 16;
+            for (int j = 1; j < 16; ++j) c[j] += __popc(x[j]);
+#ifdef CPG_CNT_SCHED
+            __builtin_amdgcn_sched_barrier(0);   // one pair's masks live at a time (registers)
+#endif
         }
-        c[15] += cstart ? 63u : 64u;
-        if (kPlus) {
-            // sign changes, position by position (rare: island borders); a loop over the
-            // block's 64-bit change mask, not inside the per-word code, so that it unrolls
-            while (ch) {
-                const int q = (int)__builtin_ctzll(ch);
-                ch &= ch - 1u;
-                const uint32_t d = (q ? base_at(w, q - 1) : wprev >> 30) * 4u + base_at(w, q);
-                const uint32_t sq = ((q < 32 ? s.x : s.y) >> (q & 31)) & 1u;
-                atomicAdd(&lds[sq ? 48u + d : 32u + d], 1u);
+        c[0] += valid ? (cstart ? 63u : 64u) : 0u;
+        // the '+' work (rare: island blocks)
+        const bool plus = valid && (s.x | s.y | sprev) != 0u;
+        if (pprep) {
+            if (plus) plus_block(w, s, wprev, sprev, cstart, lds);
+        } else if (__builtin_amdgcn_ballot_w64(plus)) {
+            plus_block(w, plus ? s : make_uint2(0u, 0u), wprev, plus ? sprev : 0u, cstart, lds);
+        }
+    }
+    // the '+'->'+' moments (the same planes masked by the '+'->'+' positions) and the sign
+    // changes, straight to LDS
+    __device__ __forceinline__ void plus_block(uint4 w, uint2 s, uint32_t wprev,
+                                               uint32_t sprev, bool cstart, uint32_t* lds) {
+        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+        const uint32_t sw[4] = {s.x & 0xFFFFu, s.x >> 16, s.y & 0xFFFFu, s.y >> 16};
+        uint32_t last = wprev;
+        uint32_t sprv = sprev & 1u;
+        uint64_t ch = 0u;   // positions whose sign differs from the previous position's
+        // both pairs' planes masked by their '+'->'+' positions (PP), then the moments one at a
+        // time (few registers live: this runs beside the counters and the loaded batches)
+        uint32_t lo[2], hi[2], plo[2], phi[2], pp[2];
+#pragma unroll
+        for (int pr = 0; pr < 2; ++pr) {
+            const uint32_t a = ww[2 * pr], b = ww[2 * pr + 1];
+            const uint32_t LO = bfi(M55, a, b << 1);
+            const uint32_t HI = bfi(M55, a >> 1, b);
+            const uint32_t PLO = __builtin_amdgcn_alignbit(LO, bfi(0x80000000u, LO << 1, last), 30);
+            const uint32_t PHI = __builtin_amdgcn_alignbit(HI, bfi(0x80000000u, HI << 1, last >> 1), 30);
+            last = b;
+            uint32_t pp2[2];
+#pragma unroll
+            for (int h = 0; h < 2; ++h) {
+                const int k = 2 * pr + h;
+                const uint32_t S = spread16(sw[k]);
+                const uint32_t Sp = (S << 2) | sprv;   // sign of the previous position
+                sprv = sw[k] >> 15;
+                pp2[h] = Sp & S;   // bit 0 of a chunk's first word: Sp = 0 (sprev = 0)
+                uint32_t chg = (Sp ^ S) & M55;
+                if (k == 0 && cstart) chg &= ~1u;
+                ch |= (uint64_t)compact16(chg) << (16 * k);
             }
+            pp[pr] = pp2[0] | (pp2[1] << 1);   // '+'->'+' transitions
+            lo[pr] = LO & pp[pr]; hi[pr] = HI & pp[pr]; plo[pr] = PLO & pp[pr]; phi[pr] = PHI & pp[pr];
+        }
+        auto mom = [&](int pr, int j) {   // moment j's mask of pair pr (j compile-time)
+            uint32_t x = pp[pr];
+            if (j & 1) x &= lo[pr];
+            if (j & 2) x &= hi[pr];
+            if (j & 4) x &= plo[pr];
+            if (j & 8) x &= phi[pr];
+            return x;
+        };
+        if (pprep) {   // lane-spread replicas [moment][lane % 16]: plain per-lane LDS atomics
+            const int col = threadIdx.x & 15;
+#pragma unroll
+            for (int j = 0; j < 16; ++j) {
+                const uint32_t v = __popc(mom(0, j)) + __popc(mom(1, j));
+                if (v) atomicAdd(&pprep[j * 16 + col], v);
+            }
+        } else {       // the whole wave is here: one reduction, one atomic per moment
+            uint32_t m[16];
+#pragma unroll
+            for (int j = 0; j < 16; ++j) m[j] = __popc(mom(0, j)) + __popc(mom(1, j));
+            wave_sum16(m, lds + 16);   // (a lane without '+' states adds zeros)
+        }
+        // sign changes, position by position (rare: island borders)
+        while (ch) {
+            const int q = (int)__builtin_ctzll(ch);
+            ch &= ch - 1u;
+            const uint32_t d = (q ? base_at(w, q - 1) : wprev >> 30) * 4u + base_at(w, q);
+            const uint32_t sq = ((q < 32 ? s.x : s.y) >> (q & 31)) & 1u;
+            atomicAdd(&lds[sq ? 48u + d : 32u + d], 1u);
         }
     }
     // base q (0..63) of a block (selects, no indexed array)
@@ -153,10 +176,18 @@ struct Lane {
         const uint32_t x = q < 32 ? (q < 16 ? w.x : w.y) : (q < 48 ? w.z : w.w);
         return (x >> (2 * (q & 15))) & 3u;
     }
-    // the wave's basis sums -> lds[0 .. 16) (all transitions) and lds[16 .. 32) ('+'->'+');
-    // every lane of the wave calls; counters re-zeroed.  Recursive halving (after 4 levels
-    // lane L holds sum L & 15 of its 16-lane row, 15 shuffles instead of 16 x 4), then the rows.
+    // the wave's moment sums -> lds[0 .. 16); every lane of the wave calls; counters
+    // re-zeroed
     __device__ __forceinline__ void flush(uint32_t* lds) {
+        wave_sum16(c, lds);
+#pragma unroll
+        for (int d = 0; d < 16; ++d) c[d] = 0u;
+    }
+    // lds[0 .. 16) += the wave's sums of c[0 .. 16) (c is clobbered).  Recursive halving (after
+    // 4 levels lane L holds sum L & 15 of its 16-lane row, 15 shuffles instead of 16 x 4), then
+    // the rows; one LDS atomic per sum (a per-lane atomic on a shared address would become the
+    // compiler's lane-by-lane reduction loop)
+    static __device__ __forceinline__ void wave_sum16(uint32_t (&c)[16], uint32_t* lds) {
         const int lane = threadIdx.x & 63;
 #pragma unroll
         for (int lvl = 0; lvl < 4; ++lvl) {
@@ -174,29 +205,34 @@ struct Lane {
         uint32_t x = c[0];
         x += (uint32_t)__shfl_xor((int)x, 16);
         x += (uint32_t)__shfl_xor((int)x, 32);
-        if (lane < 16) {
-            if (x & 0xFFFFu) atomicAdd(&lds[lane], x & 0xFFFFu);
-            if (x >> 16) atomicAdd(&lds[16 + lane], x >> 16);
-        }
-#pragma unroll
-        for (int d = 0; d < 16; ++d) c[d] = 0u;
+        if (lane < 16 && x) atomicAdd(&lds[lane], x);
     }
 };
 
+// lds[16 .. 32) += the lane-spread '+'->'+' replicas (Lane::pprep), threads t < 16, after a
+// workgroup barrier
+__device__ __forceinline__ void pp_replicas_sum(const uint32_t* pprep, uint32_t* lds, int t) {
+    if (t < 16) {
+        uint32_t v = 0u;
+#pragma unroll
+        for (int i = 0; i < 16; ++i) v += pprep[t * 16 + ((i + t) & 15)];   // rotated: no conflicts
+        lds[16 + t] += v;
+    }
+}
+
 // raw sum i (< kRaw, the accumulators' layout tot[16] pp[16] pm[16] mp[16] init[8]) from a
-// workgroup's LDS counters: tot and pp from their basis (Lane), exact integer identities
+// workgroup's LDS counters: tot and pp from their moments (Lane) by Moebius inversion — the
+// cell d = p * 4 + b has exactly the planes of the bits of d (bit 0 lo, 1 hi of b; 2 lo, 3 hi
+// of p), so N(d) = sum over S containing d of (-1)^|S \ d| m_S, m_0 = the transitions (exact
+// integer identities, modulo 2^32 with a non-negative result)
 __device__ __forceinline__ uint32_t raw_of(const uint32_t* lds, int i) {
     if (i >= 32) return lds[i];
     const uint32_t* B = lds + (i & 16);
-    const int p = (i & 15) >> 2, b = i & 3;
-    if (p < 3 && b < 3) return B[p * 3 + b];
-    if (p < 3) return B[9 + p] - B[p * 3] - B[p * 3 + 1] - B[p * 3 + 2];
-    if (b < 3) return B[12 + b] - B[b] - B[3 + b] - B[6 + b];
-    uint32_t v = B[15];
+    const int d = i & 15;
+    uint32_t v = 0u;
 #pragma unroll
-    for (int j = 0; j < 9; ++j) v += B[j];
-#pragma unroll
-    for (int j = 9; j < 15; ++j) v -= B[j];
+    for (int S = 0; S < 16; ++S)
+        if ((S & d) == d) v += (__popc((uint32_t)(S ^ d)) & 1) ? 0u - B[S] : B[S];
     return v;
 }
 

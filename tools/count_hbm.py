@@ -1,0 +1,104 @@
+"""The labelled-count kernel (cpg_count_labelled_d) on an HBM-resident genome:
+event-timed launches over a buffer far larger than the 256 MB Infinity Cache (default the
+3.1 Gbp C3 genome: 775 MB packed + 388 MB label bits), set against a plain streaming read of
+the same bytes on the same box (tools/readsweep.hip).  Prints one JSON line.
+
+usage: python tools/count_hbm.py [--bases N] [--reps R] [--train]   (GPU; dev tool)
+"""
+import argparse
+import ctypes as C
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+import numpy as np  # noqa: E402
+import torch  # noqa: E402
+
+from cpgisland_amd import Context, HmmModel  # noqa: E402
+from cpgisland_amd import device as D  # noqa: E402
+
+TRAIN = 65536
+
+
+def timed(fn, reps):
+    ts = []
+    for _ in range(reps):
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        fn()
+        b.record()
+        ts.append((a, b))
+    torch.cuda.synchronize()
+    ms = sorted(a.elapsed_time(b) for a, b in ts)
+    return ms[len(ms) // 2], ms[0]
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--bases", type=int, default=3_100_000_000)
+    ap.add_argument("--reps", type=int, default=20)
+    ap.add_argument("--train", action="store_true", help="also time the fused training pass")
+    ap.add_argument("--no-sweep", action="store_true")
+    a = ap.parse_args()
+    N = a.bases // TRAIN * TRAIN
+    dev = torch.device("cuda:0")
+    t0 = time.time()
+    packed, sign = D.synth_host(20251015 + 2, 0, N)
+    print(f"synth {N} bases {time.time() - t0:.1f}s", file=sys.stderr, flush=True)
+    dp, ds = D.to_device(packed, dev), D.to_device(sign, dev)
+    del packed, sign
+    ctx = Context(0)
+    ctx.reserve(min(N, 1 << 28))
+    out = torch.empty(124, dtype=torch.int64, device=dev)
+    for _ in range(3):
+        D.count_labelled(ctx, dp, ds, N, TRAIN, out=out)
+    torch.cuda.synchronize()
+    ctx.sync()
+    c = out.cpu().numpy()
+    nch = N // TRAIN
+    ok = bool(c[:8].sum() == nch and c[8:72].sum() == nch * (TRAIN - 1)
+              and c[120:124].sum() == N and c[104:120].sum() == nch * (TRAIN - 1))
+    med, best = timed(lambda: D.count_labelled(ctx, dp, ds, N, TRAIN, out=out), a.reps)
+    alg = 0.375 * N
+    res = {"tool": "count_hbm", "bases": N, "algorithmic_bytes": alg,
+           "count_ms_median": med, "count_ms_best": best,
+           "count_GBps_median": alg / med / 1e6, "count_frac_of_8TBps": alg / med / 1e6 / 8000,
+           "identities_ok": ok}
+    if a.train:
+        m0 = HmmModel.initial()
+        eo = torch.empty(105, dtype=torch.float64, device=dev)
+        for _ in range(2):
+            D.train_pass(ctx, m0, dp, ds, N, TRAIN, estep_out=eo, counts_out=out)
+        tm, tb = timed(lambda: D.train_pass(ctx, m0, dp, ds, N, TRAIN, estep_out=eo, counts_out=out),
+                       max(3, a.reps // 4))
+        res.update({"train_pass_ms_median": tm, "train_pass_Gbase_s": N / tm / 1e6})
+    if not a.no_sweep:
+        so = os.path.join(ROOT, "tools", "libreadsweep.so")
+        lib = C.CDLL(so)
+        lib.readsweep.argtypes = [C.c_void_p, C.c_int64, C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        sink = torch.zeros(4, dtype=torch.int32, device=dev)
+        st = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+        nbp, nbs = N // 4, N // 8
+        best_sw = None
+        for grid in (1024, 2048, 4096, 8192):
+            for inf in (2, 4, 8):
+                def sweep():
+                    lib.readsweep(C.c_void_p(dp.data_ptr()), nbp, C.c_void_p(sink.data_ptr()), grid, inf, st)
+                    lib.readsweep(C.c_void_p(ds.data_ptr()), nbs, C.c_void_p(sink.data_ptr()), grid, inf, st)
+                sweep()
+                m, _ = timed(sweep, max(5, a.reps // 2))
+                r = (nbp + nbs) / m / 1e6
+                if best_sw is None or r > best_sw[0]:
+                    best_sw = (r, grid, inf, m)
+        res.update({"readsweep_GBps": best_sw[0], "readsweep_grid": best_sw[1],
+                    "readsweep_inflight": best_sw[2], "readsweep_ms": best_sw[3],
+                    "count_vs_readsweep": res["count_GBps_median"] / best_sw[0]})
+    ctx.close()
+    print(json.dumps(res), flush=True)
+
+
+if __name__ == "__main__":
+    main()

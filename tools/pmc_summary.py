@@ -50,6 +50,7 @@ for k in sorted(vals, key=lambda k: -sum(dur.get(k, [0]))):
               "traffic_bytes": fetch + write, **{c: v[c] for c in v}}
 if len(sys.argv) > 2:
     import time
+    what = sys.argv[4] if len(sys.argv) > 4 else "bench.py --serial"
     json.dump({"bases": int(sys.argv[3]) if len(sys.argv) > 3 else None,
-               "collected": time.strftime("%Y-%m-%d") + " tools/pmc.sh (bench.py --serial)",
+               "collected": time.strftime("%Y-%m-%d") + " tools/pmc_round.sh (" + what + ")",
                "kernels": out}, open(sys.argv[2], "w"), indent=1, sort_keys=True)

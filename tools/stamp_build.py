@@ -12,7 +12,7 @@ SRC = os.path.join(R, "cpgisland_amd", "csrc")
 TREE = os.path.join(R, "build", "abl", "stamp_tree")        # csrc + include, same relative layout
 DST = os.path.join(TREE, "cpgisland_amd", "csrc")
 HEAD = '''__device__ unsigned long long g_stamp[2048 * 12];
-#define STAMP(i) do { if (threadIdx.x == 0) g_stamp[blockIdx.x * 12 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define STAMP(i) do { if (threadIdx.x == 0 && blockIdx.x < 2048) g_stamp[blockIdx.x * 12 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 '''
 TAIL = '''
 namespace cpg {
@@ -22,7 +22,7 @@ extern "C" int cpg_dbg_stamps(unsigned long long* h, int n) {
 }
 '''
 K4HEAD = """__device__ unsigned long long g_stamp4[1024 * 8];
-#define STAMP4(i) do { if (threadIdx.x == 0) g_stamp4[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
+#define STAMP4(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_stamp4[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
 """
 K4TAIL = """
 namespace cpg {
@@ -84,7 +84,7 @@ def main():
     base = ("-O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function "
             "-Wno-unused-variable --offload-arch=gfx950 -munsafe-fp-atomics " + os.environ.get("STAMP_FLAGS", ""))
     subprocess.run(["make", "-s", "-j8", "-C", DST, "OBJDIR=../../obj",
-                    f"OUT={os.path.join(R, 'build', 'abl', 'libcpg_stamp.so')}", f"CXXFLAGS={base}", os.path.join(R, "build", "abl", "libcpg_stamp.so")],
+                    f"OUT={os.path.join(R, 'build', 'abl', os.environ.get('STAMP_OUT', 'libcpg_stamp.so'))}", f"CXXFLAGS={base}", os.path.join(R, 'build', 'abl', os.environ.get('STAMP_OUT', 'libcpg_stamp.so'))],
                    check=True)
 
 
