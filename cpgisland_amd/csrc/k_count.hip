@@ -56,7 +56,7 @@ __device__ __forceinline__ void load_batch(Batch& b, const uint4* __restrict__ p
                                            const uint2* __restrict__ sign2,
                                            const uint32_t* __restrict__ packed,
                                            const uint32_t* __restrict__ sign, int64_t g,
-                                           int lane, uint32_t stride, int64_t nblk) {
+                                           int lane, uint32_t stride, int64_t nblk, uint32_t zv) {
     const int64_t lim64 = nblk - 1 - g;   // wave-uniform; >= 0 for the rounds that count
     const uint32_t lim = lim64 < 0 ? 0u : lim64 > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)lim64;
     const uint4* pb = packed4 + min(g, nblk - 1);
@@ -67,9 +67,13 @@ __device__ __forceinline__ void load_batch(Batch& b, const uint4* __restrict__ p
         const uint32_t o = min((uint32_t)lane + (uint32_t)r * stride, lim) * base_ok;
         b.w[r] = pb[o];
         b.s[r] = sb[o];
+        // (zv: an opaque zero in a VGPR, so that these wave-uniform loads stay VECTOR loads,
+        // counted in order with the batch's other loads: as scalar loads they made every
+        // batch wait lgkmcnt(0) — for the NEXT batch's scalar loads too, which SMEM returns
+        // out of order)
         const int64_t ip = min(max(g + (int64_t)r * stride - 1, (int64_t)0), nblk - 1);
-        b.wp0[r] = packed[4 * ip + 3];
-        b.sp0[r] = sign[2 * ip + 1];
+        b.wp0[r] = packed[4 * ip + 3 + zv];
+        b.sp0[r] = sign[2 * ip + 1 + zv];
     }
 }
 
@@ -123,14 +127,16 @@ void k_count_main(const uint4* __restrict__ packed4, const uint2* __restrict__ s
         if (gb + span < nblk) count(b, gb, std::false_type{});
         else count(b, gb, std::true_type{});
     };
+    uint32_t zv;
+    asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
     Batch A, B;
-    load_batch(A, packed4, sign2, packed, sign, g, lane, stride, nblk);
+    load_batch(A, packed4, sign2, packed, sign, g, lane, stride, nblk, zv);
     while (g < nblk) {
-        load_batch(B, packed4, sign2, packed, sign, g + step, lane, stride, nblk);
+        load_batch(B, packed4, sign2, packed, sign, g + step, lane, stride, nblk, zv);
         count_round(A, g);
         g += step;
         if (g < nblk) {
-            load_batch(A, packed4, sign2, packed, sign, g + step, lane, stride, nblk);
+            load_batch(A, packed4, sign2, packed, sign, g + step, lane, stride, nblk, zv);
             count_round(B, g);
             g += step;
         }

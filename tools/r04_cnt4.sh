@@ -10,7 +10,7 @@ hbm() {
   echo "$1 $(python3 -c "import json; d=json.load(open('$OUT/$1.json')); print(round(d['count_ms_median'],4), round(d['count_GBps_median']), d.get('train_pass_ms_median'))")"
 }
 hbm default $R/cpgisland_amd/libcpg.so --train || exit 1
-for v in ${VARIANTS:-q1g2048 q1g4096 q2g1024}; do hbm $v $R/build/abl/libcpg_$v.so || exit 1; done
+for v in ${VARIANTS:-r2g2048 r1g1024 r1g4096}; do hbm $v $R/build/abl/libcpg_$v.so || exit 1; done
 cd /tmp && export TMPDIR=/tmp
 timeout -k 10 120 rocprofv3 --pmc SQ_WAVES SQ_INSTS_VALU SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_WAVE_CYCLES SQ_ACTIVE_INST_VALU SQ_WAIT_ANY SQ_WAIT_INST_ANY --kernel-trace --output-format csv -d $OUT/pmc/p1 -o p1 \
   -- python $R/tools/count_hbm.py --bases 3100000000 --no-sweep --reps 3 > /dev/null 2> $OUT/p1.err || { tail -3 $OUT/p1.err; exit 1; }
