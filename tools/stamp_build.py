@@ -21,22 +21,6 @@ extern "C" int cpg_dbg_stamps(unsigned long long* h, int n) {
 }
 }
 '''
-K4HEAD = """__device__ unsigned long long g_stamp4[1024 * 8];
-#define STAMP4(i) do { if (threadIdx.x == 0 && blockIdx.x < 1024) g_stamp4[blockIdx.x * 8 + (i)] = __builtin_amdgcn_s_memrealtime(); } while (0)
-"""
-K4TAIL = """
-namespace cpg {
-extern "C" int cpg_dbg_stamps4(unsigned long long* h, int n) {
-    return (int)hipMemcpyFromSymbol(h, HIP_SYMBOL(g_stamp4), (size_t)n * 8);
-}
-}
-"""
-K4ANCHORS = [("    const int64_t s0 = c * nseg;", 0),
-             ("    // B. gap composites and windows, one lane per barrier.", 1),
-             ("    const int nst = min(nbar, kMaxStagedBar);\n    C64 Rg", 2),
-             ("    const bool all_staged = nst == nbar", 3),
-             ("    // D. anchor values by block id", 4),
-             ("        else ent[g.nsb] = E;\n    }\n", 5)]
 # (anchor, stamp index, before|after): the phase boundaries of k_estep_chunk
 ANCHORS = [
     ("    const uint32_t* pk = packed + c * (C / 16);\n", 0, "after"),
@@ -68,18 +52,6 @@ def main():
     s = s.replace("        reset_done(done);\n    }\n}", "        reset_done(done);\n    }\n    STAMP(11);\n}", 1)
     s = s.replace("    STAMP(7);\n", "    STAMP(7);\n    STAMP(8);\n", 1)
     s += TAIL
-    open(p, "w").write(s)
-    # K4 (k_vit_chain_seg): one stamp row per chunk (workgroup), thread 0
-    p = os.path.join(DST, "k_viterbi.hip")
-    s = open(p).read()
-    s = s.replace("namespace cpg {\nnamespace {\n", "namespace cpg {\nnamespace {\n" + K4HEAD, 1)
-    a = s.index("__global__ __launch_bounds__(kSegT) void k_vit_chain_seg(")
-    body = s[a:]
-    for anchor, i in K4ANCHORS:
-        assert anchor in body, anchor
-        st = f"    STAMP4({i});\n"
-        body = body.replace(anchor, anchor + st if i == 5 else st + anchor, 1)
-    s = s[:a] + body + K4TAIL
     open(p, "w").write(s)
     base = ("-O3 -std=c++17 -fPIC -ffp-contract=off -Wall -Wno-unused-function "
             "-Wno-unused-variable --offload-arch=gfx950 -munsafe-fp-atomics " + os.environ.get("STAMP_FLAGS", ""))
