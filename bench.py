@@ -40,6 +40,8 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # lane products 4 two-by-two products per 16 positions = 3 — implementation recomputation
 # (the second forward pass over half of each mini-block) not counted
 FP64_PEAK_TFLOPS = 78.6
+# the training pass's kernel (the E-step chunk kernel; its kCnt instantiation in the fused pass)
+ESTEP_KERNEL = "k_estep_chunk"
 ESTEP_FLOPS_PER_BASE = 23
 # algorithmic bytes per base of each phase: the fused
 # decode (cpg_decode_d) reads the packed bases once and writes the 1-bit path (0.375); the
@@ -509,7 +511,7 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
                           "islands_found": sum(counts)},
                "phases_ms": {"train_pass": round(tr_ms, 4)},
                "host_issue_ms_per_step": round(issue * 1e3 / args.steps, 4),
-               "roofline": {"bound": "hbm", "kernel": "k_estep_chunk<true>", "phase": "train_pass",
+               "roofline": {"bound": "hbm", "kernel": ESTEP_KERNEL, "phase": "train_pass",
                             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                             "algorithmic_bytes": bpb * tr_n, "bytes_per_base": bpb},
@@ -519,7 +521,7 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
                                      "oracle on a bounded sample of the same synthetic genome")}
         # HBM traffic of the training pass at this rank's size: the PMC profile of the C3
         # workload on one GPU (tools/pmc.sh c3), scaled to the shard's bases
-        pmc = _pmc_traffic("k_estep_chunk", tr_n, name="pmc_c3.json", scale=True)
+        pmc = _pmc_traffic(ESTEP_KERNEL, tr_n, name="pmc_c3.json", scale=True)
         if pmc:
             out["roofline"]["traffic"] = pmc["traffic_bytes"]
             out["roofline"]["traffic_source"] = "stored PMC profile, not this run: " + pmc["source"]
@@ -987,12 +989,12 @@ def main():
         alg_bytes = bpb * N
         ach = alg_bytes / (phases[dom] / 1e3) / 1e9 if phases[dom] > 0 else 0.0
         roof = {"bound": "hbm",
-                "kernel": ("k_estep_chunk<true> (training pass: E-step + labelled counts)"
-                           if fused else "k_estep_chunk"), "phase": dom,
+                "kernel": (ESTEP_KERNEL + " (training pass: E-step + labelled counts)"
+                           if fused else ESTEP_KERNEL), "phase": dom,
                 "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                 "algorithmic_bytes": alg_bytes, "bytes_per_base": bpb}
-        pmc = _pmc_traffic("k_estep_chunk", N)
+        pmc = _pmc_traffic(ESTEP_KERNEL, N)
         if pmc:
             roof["traffic"] = pmc["traffic_bytes"]
             roof["traffic_source"] = ("stored PMC profile, not this run: " + pmc["source"])
@@ -1004,7 +1006,7 @@ def main():
         # the limiter named above, priced: algorithmic fp64 flops per launch / the same phase
         # time, against the fp64 vector peak
         fl = ESTEP_FLOPS_PER_BASE * N / (phases[dom] / 1e3) / 1e12 if phases[dom] > 0 else 0.0
-        roof_fp64 = {"bound": "valu-fp64", "kernel": "k_estep_chunk", "phase": dom,
+        roof_fp64 = {"bound": "valu-fp64", "kernel": ESTEP_KERNEL, "phase": dom,
                      "achieved": round(fl, 2), "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(fl / FP64_PEAK_TFLOPS, 4),
                      "flops_per_base": ESTEP_FLOPS_PER_BASE}

@@ -35,6 +35,23 @@ __global__ void k_op(unsigned* out, long long* cyc, unsigned a, unsigned b) {
             if (OP == 6) x[c] = x[c] & y;                                   // v_and_b32
             if (OP == 7) asm volatile("v_bfi_b32 %0, %1, %2, %3" : "=v"(x[c]) : "v"(x[c]), "v"(y), "v"(z));
             if (OP == 8) x[c] = (x[c] << 1) | y;                            // v_lshl_or_b32
+            if (OP >= 9) {   // 64-bit ops on (x[c], y) pairs: the K5 step's candidates
+                const unsigned long long a = ((unsigned long long)y << 32) | x[c];
+                const unsigned long long b = ((unsigned long long)z << 32) | x[(c + 3) % NC];
+                unsigned long long r;
+                if (OP == 9) r = a + b;                                          // v_lshl_add_u64
+                if (OP == 10) r = (long long)a > (long long)b ? a : b;            // cmp_i64 + 2 cndmask
+                if (OP == 11) {                                                   // v_add_f64
+                    const double d = __longlong_as_double((long long)a) + __longlong_as_double((long long)b);
+                    r = (unsigned long long)__double_as_longlong(d);
+                }
+                if (OP == 12) {                                                   // v_max_f64
+                    const double d = fmax(__longlong_as_double((long long)a), __longlong_as_double((long long)b));
+                    r = (unsigned long long)__double_as_longlong(d);
+                }
+                if (OP == 13) r = a + (__longlong_as_double((long long)a) > __longlong_as_double((long long)b) ? 1 : 0);   // v_cmp_gt_f64 (+ addc)
+                x[c] = (unsigned)r ^ (unsigned)(r >> 32);
+            }
         }
     }
     __syncthreads();
@@ -80,6 +97,11 @@ int main() {
         run<6>("and", th);
         run<7>("bfi", th);
         run<8>("lshl_or", th);
+        run<9>("add_u64", th);
+        run<10>("max_i64", th);
+        run<11>("add_f64", th);
+        run<12>("max_f64", th);
+        run<13>("cmp_f64", th);
     }
     return 0;
 }
