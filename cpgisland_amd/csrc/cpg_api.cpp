@@ -498,7 +498,7 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
     unsigned int* done = static_cast<unsigned int*>(dn);
     // fused: the traceback writes the island run records and a chunk's last traceback
     // workgroup resolves it — no island kernels
-    if (islands_fusable(nch, chunk_len)) {
+    if (islands_fusable(nch, chunk_len) && tail_fusion_pays(nch)) {
         IslFuse fz;
         CPG_HIP(islands_fuse(&fz, wsi, ctx->ws[WS_ISL].bytes, nch, chunk_len, first_chunk, d_out,
                              cap, d_count, ctx->d_status, static_cast<unsigned long long*>(fl),

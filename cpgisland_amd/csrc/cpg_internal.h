@@ -224,6 +224,16 @@ size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
 // fused decode (cpg_decode_d): the traceback writes the island tile lists and a chunk's last
 // traceback workgroup resolves it (no island kernels); done: nchunks zeroed words (WS_IDONE)
 bool islands_fusable(int64_t nchunks, int64_t chunk_len);
+// Per-chunk tail work folded into the last workgroup of a chunk (K6 into K5, the island tiles
+// and the chunk resolve into K7) pays while the chunks are few: it saves a launch and the
+// grid-wide boundary, and the tails run on an otherwise draining GPU.  With many chunks the
+// GPU is full when each tail runs, so a latency-bound tail shares a busy CU: at 2,956 chunks
+// (3.1 Gbp) K5 + K6 as two launches took 1,269 against 1,365 us and the separate traceback +
+// tile + resolve kernels 648 against 1,013 us (decode 3.735 against 4.040 ms); at 43 chunks
+// the fused decode is 4 % faster, at 256 they are equal, at 1,024 the separate one 3 %
+// faster (profiles/r04_dec2/).  One chunk per compute unit is the crossover.
+constexpr int64_t kTailFuseMaxChunks = 256;
+inline bool tail_fusion_pays(int64_t nchunks) { return nchunks <= kTailFuseMaxChunks; }
 hipError_t islands_fuse(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
                         int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
                         int64_t* count, uint32_t* status, unsigned long long* flags,

@@ -197,7 +197,7 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
         if (decode) {
             if (k >= nbuf) CPG_HIP(hipStreamWaitEvent(sdec, ev_out[b], 0));
             if (nd > 0) {
-                if (islands_fusable(nd, D)) {   // fused decode (as cpg_decode_d)
+                if (islands_fusable(nd, D) && tail_fusion_pays(nd)) {   // fused decode (as cpg_decode_d)
                     IslFuse fz;
                     CPG_HIP(islands_fuse(&fz, ws_isl, ctx->ws[WS_ISL].bytes, nd, D,
                                          chunk0 + start / D, d_isl, island_cap, d_icnt + k + 1,

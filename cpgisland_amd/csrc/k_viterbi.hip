@@ -49,12 +49,6 @@
 namespace cpg {
 namespace {
 
-#ifndef CPG_K3_PRIV
-#define CPG_K3_PRIV 0
-#endif
-#ifndef CPG_K6_SEP
-#define CPG_K6_SEP 0
-#endif
 constexpr int kThreads = 256;
 constexpr int kMaxSeg = 16;   // segment path: 256-block segments per chunk (chunks up to 1 Mi)
 constexpr int32_t kNeg32 = -(1 << 30);
@@ -753,21 +747,12 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     const bool four = s_emin == s_emax;   // workgroup-uniform
     if (s_part) load_single();   // (tables only where a workgroup uses them: ~11 KB each)
     if (four) {
-#if CPG_K3_PRIV   // (measurement variant) lane-private 2-step rows: conflict-free reads
-        const double2* ga = dv->P2A + (size_t)s_emin * 64;
-        const double2* gb = dv->P2B + (size_t)s_emin * 64;
-        for (int i = threadIdx.x; i < 64 * 16; i += kThreads) {
-            P4A[i] = ga[i >> 4];
-            P4B[i] = gb[i >> 4];
-        }
-#else
         const double2* ga = dv->P4A + (size_t)s_emin * kW4;
         const double2* gb = dv->P4B + (size_t)s_emin * kW4;
         for (int i = threadIdx.x; i < kW4; i += kThreads) {
             P4A[i] = ga[i];
             P4B[i] = gb[i];
         }
-#endif
     } else {
         for (int i = threadIdx.x; i < nb * 64; i += kThreads) {
             P2A[i] = dv->P2A[vc.emin * 64 + i];
@@ -782,25 +767,6 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     if (!reg) {
     } else if (g.full(k) && four) {
         const BlockWords bw = load_block(pk, k);
-#if CPG_K3_PRIV
-        const double2* pa = P4A + (threadIdx.x & 15);
-        const double2* pb = P4B + (threadIdx.x & 15);
-        C64 half = c64_id();
-        pipelined<4, 128>(
-            [&](int j) {   // 3-base window of steps 2j, 2j+1
-                const int r = j >> 3, s = j & 7;
-                const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
-                return s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 63u)
-                              : ((bw.w[r] >> (4 * s - 2)) & 63u);
-            },
-            [&](uint32_t wi) {
-                return C64{pa[wi * 16].x, pa[wi * 16].y, pb[wi * 16].x, pb[wi * 16].y};
-            },
-            [&](const C64& m, int j) {
-                if (j & 1) acc = c64_mul(acc, c64_mul(half, m));
-                else half = m;
-            });
-#else
         pipelined<4, 64>(
             [&](int j) {   // 5-base window of steps 4j .. 4j+3
                 const int r = j >> 2, s = j & 3;
@@ -810,7 +776,6 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
             },
             [&](uint32_t wi) { return C64{P4A[wi].x, P4A[wi].y, P4B[wi].x, P4B[wi].y}; },
             [&](const C64& m, int) { acc = c64_mul(acc, m); });
-#endif
     } else if (g.full(k)) {
         const double2* pa = P2A + slot * 64;
         const double2* pb = P2B + slot * 64;
@@ -2302,8 +2267,9 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
         hipLaunchKernelGGL(k_vit_chain, dim3((unsigned)nchunks), dim3(kChainT), 0, s, vc, packed,
                            g, w.plan, w.comp3, w.degen, w.entry, w.gk, w.gap, w.barlist, w.vout,
                            w.vhead);
-    // chunks of whole K5 workgroups: the trace scan runs in each chunk's last K5 workgroup
-    if (done5 && nsb % kThreads == 0 && !CPG_K6_SEP) {
+    // chunks of whole K5 workgroups: the trace scan runs in each chunk's last K5 workgroup —
+    // while the chunks are few (tail_fusion_pays); past that, as its own launch
+    if (done5 && nsb % kThreads == 0 && tail_fusion_pays(nchunks)) {
         hipLaunchKernelGGL(k_vit_forward<true>, dim3(grid), dim3(kThreads), 0, s, vc, packed, g,
                            w.degen, w.entry, w.bp, w.origin, status, w.gk, sg, w.went, done5,
                            w.endst, score);
