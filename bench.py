@@ -394,6 +394,13 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
                                    torch.cuda.Stream(), torch.cuda.Stream())
     ev = {k: [torch.cuda.Event() for _ in range(2)] for k in
           ("halo", "tr_done", "dec_done", "rec", "red", "isl")}
+    # several ranks on ONE GPU (the CPG_BENCH_BACKEND=gloo rehearsal on a one-GPU box): the
+    # decode's look-back kernels (the island resolve, K1's segment look-back) spin on flags of
+    # earlier workgroups of their own launch, which is safe for one launch but not for two
+    # processes' launches sharing the CUs — each can hold every slot spinning while the other's
+    # awaited workgroups wait for one.  The ranks then take turns for the decode (host
+    # barriers: a rehearsal of the code path, not a rate); one process per GPU never does this.
+    shared = bool(dist) and torch.cuda.device_count() < world
     ntr = []   # (start, end) timing events of the training pass, every 4th timed step
 
     # the decode model: one Baum-Welch iteration over the whole genome from the reference's
@@ -434,8 +441,14 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
             s_dec.wait_event(ev["halo"][b])
             if k >= 2:
                 s_dec.wait_event(ev["isl"][b])   # step k-2's island gather has read the records
-            D.decode(ctx, model1, bp[de_o // 16:], de_n, DECODE, cap=icap, first_chunk=pl.d0,
-                     sign_out=so, score=score, out=iout[b], count=icnt[b])
+            for r in (range(world) if shared else (rank,)):
+                if r == rank:
+                    D.decode(ctx, model1, bp[de_o // 16:], de_n, DECODE, cap=icap,
+                             first_chunk=pl.d0, sign_out=so, score=score, out=iout[b],
+                             count=icnt[b])
+                if shared:   # ranks sharing one GPU (the gloo rehearsal) take turns
+                    s_dec.synchronize()
+                    torch.distributed.barrier()
             ev["dec_done"][b].record(s_dec)
         with torch.cuda.stream(s_tr):
             s_tr.wait_event(ev["halo"][b])
@@ -508,6 +521,7 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
                                           if dist else None),
                           "train_cus": ntc or ncu,
                           "decode_priority": "high" if args.prio else "normal",
+                          "ranks_share_gpu": shared,
                           "islands_found": sum(counts)},
                "phases_ms": {"train_pass": round(tr_ms, 4)},
                "host_issue_ms_per_step": round(issue * 1e3 / args.steps, 4),
