@@ -49,9 +49,6 @@
 namespace cpg {
 namespace {
 
-#ifndef CPG_K3_L1
-#define CPG_K3_L1 0
-#endif
 constexpr int kThreads = 256;
 constexpr int kMaxSeg = 16;   // segment path: 256-block segments per chunk (chunks up to 1 Mi)
 constexpr int32_t kNeg32 = -(1 << 30);
@@ -694,16 +691,11 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     // block instead of 128) or the 2-step composites of every binade
     extern __shared__ __attribute__((aligned(16))) double2 sLe[];
     const int nb = vc.emax - vc.emin + 1;
-#if CPG_K3_L1   // (measurement variant) segment path: one 32 KB union, multi-binade rows from L1
-    const bool compact = seg != nullptr;   // (no partial blocks on the segment path)
-#else
-    constexpr bool compact = false;
-#endif
     double2* sA = sLe;
     double2* sB = sA + nb * 16;
     double2* P2A = sB + nb * 16;
     double2* P2B = P2A + nb * 64;
-    double2* P4A = compact ? sLe : sB + nb * 16;
+    double2* P4A = sB + nb * 16;
     double2* P4B = P4A + kW4;
     __shared__ int s_emin, s_emax, s_part;
     const VitDerived* dv = derived(vt);
@@ -761,7 +753,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
             P4A[i] = ga[i];
             P4B[i] = gb[i];
         }
-    } else if (!compact) {
+    } else {
         for (int i = threadIdx.x; i < nb * 64; i += kThreads) {
             P2A[i] = dv->P2A[vc.emin * 64 + i];
             P2B[i] = dv->P2B[vc.emin * 64 + i];
@@ -785,8 +777,8 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
             [&](uint32_t wi) { return C64{P4A[wi].x, P4A[wi].y, P4B[wi].x, P4B[wi].y}; },
             [&](const C64& m, int) { acc = c64_mul(acc, m); });
     } else if (g.full(k)) {
-        const double2* pa = compact ? dv->P2A + (size_t)p.e_pre * 64 : P2A + slot * 64;
-        const double2* pb = compact ? dv->P2B + (size_t)p.e_pre * 64 : P2B + slot * 64;
+        const double2* pa = P2A + slot * 64;
+        const double2* pb = P2B + slot * 64;
         const BlockWords bw = load_block(pk, k);
         pipelined<4, 128>(
             [&](int j) {   // 3-base window of steps 2j, 2j+1
@@ -2260,12 +2252,7 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                            packed, g, w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount,
                            w.vhead);
     const size_t nbz = (size_t)(vc.emax - vc.emin + 1);
-#if CPG_K3_L1
-    const size_t lds3x = segp ? std::max((size_t)kW4 * 2, nbz * 16 * 2) * sizeof(double2)
-                              : (nbz * 16 * 2 + std::max(nbz * 64 * 2, (size_t)kW4 * 2)) * sizeof(double2);
-#else
     const size_t lds3x = (nbz * 16 * 2 + std::max(nbz * 64 * 2, (size_t)kW4 * 2)) * sizeof(double2);
-#endif
     // K3 + K3b in one launch: the chunks' irregular blocks run as extra workgroups (segment
     // path: and block 0's walks, one lane per chunk)
     const unsigned heads3 = segp ? (unsigned)((nchunks + kThreads - 1) / kThreads) : 0u;

@@ -26,3 +26,6 @@ PY
 }
 run new $L || exit 1; run k3l1 $V || exit 1; run new_b $L || exit 1; run k3l1_b $V || exit 1
 run new46 $L 46000000 || exit 1; run k3l146 $V 46000000 || exit 1
+# K5 built for 6 waves per SIMD (71 VGPRs, no spills) instead of 8 (64, 10 spills)
+K5=$R/build/abl/libcpg_k5w6.so
+[ -f $K5 ] && { run k5w6 $K5 || exit 1; run k5w6_46 $K5 46000000 || exit 1; }
