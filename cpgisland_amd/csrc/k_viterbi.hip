@@ -691,11 +691,16 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
     // block instead of 128) or the 2-step composites of every binade
     extern __shared__ __attribute__((aligned(16))) double2 sLe[];
     const int nb = vc.emax - vc.emin + 1;
+    // segment path (no partial blocks): ONE 32 KB union holds the table the workgroup uses —
+    // the single-step rows (irregular-block workgroups), the 4-step composites of one binade,
+    // or the 2-step rows of the segment's binade range only — 4 workgroups per CU instead of
+    // 3 (K3 1.23 -> 1.15 ms at 3.1 Gbp, profiles/r04_k3range/)
+    const bool compact = seg != nullptr;
     double2* sA = sLe;
     double2* sB = sA + nb * 16;
-    double2* P2A = sB + nb * 16;
+    double2* P2A = compact ? sLe : sB + nb * 16;
     double2* P2B = P2A + nb * 64;
-    double2* P4A = sB + nb * 16;
+    double2* P4A = compact ? sLe : sB + nb * 16;
     double2* P4B = P4A + kW4;
     __shared__ int s_emin, s_emax, s_part;
     const VitDerived* dv = derived(vt);
@@ -753,16 +758,26 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
             P4A[i] = ga[i];
             P4B[i] = gb[i];
         }
-    } else {
+    } else if (!compact) {
         for (int i = threadIdx.x; i < nb * 64; i += kThreads) {
             P2A[i] = dv->P2A[vc.emin * 64 + i];
             P2B[i] = dv->P2B[vc.emin * 64 + i];
         }
     }
+    // compact: the 2-step rows of the segment's binade range only (<= 16 binades: 32 KB)
+    const int nrange = s_emax - s_emin + 1;
+    const bool glob2 = compact && !four && nrange > kW4 / 64;   // (rows from device memory)
+    if (compact && !four && !glob2 && nrange > 0) {
+        P2B = P2A + nrange * 64;
+        for (int i = threadIdx.x; i < nrange * 64; i += kThreads) {
+            P2A[i] = dv->P2A[(size_t)s_emin * 64 + i];
+            P2B[i] = dv->P2B[(size_t)s_emin * 64 + i];
+        }
+    }
     __syncthreads();
     if (!reg && !seg) return;   // (segment path: every lane takes part in the scan below)
     const uint32_t* pk = chunk_ptr(packed, g, c);
-    const int slot = p.e_pre - vc.emin;
+    const int slot = p.e_pre - (compact ? s_emin : vc.emin);
     C64 acc = c64_id();
     if (!reg) {
     } else if (g.full(k) && four) {
@@ -775,6 +790,19 @@ __global__ __launch_bounds__(kThreads) void k_vit_exact(VitConsts vc, const VitT
                               : ((bw.w[r] >> (8 * s - 2)) & 0x3FFu);
             },
             [&](uint32_t wi) { return C64{P4A[wi].x, P4A[wi].y, P4B[wi].x, P4B[wi].y}; },
+            [&](const C64& m, int) { acc = c64_mul(acc, m); });
+    } else if (g.full(k) && glob2) {
+        const double2* pa = dv->P2A + (size_t)p.e_pre * 64;
+        const double2* pb = dv->P2B + (size_t)p.e_pre * 64;
+        const BlockWords bw = load_block(pk, k);
+        pipelined<4, 128>(
+            [&](int j) {   // 3-base window of steps 2j, 2j+1
+                const int r = j >> 3, s = j & 7;
+                const uint32_t lo = r == 0 ? bw.prev : bw.w[r - 1];
+                return s == 0 ? (__builtin_amdgcn_alignbit(bw.w[r], lo, 30) & 63u)
+                              : ((bw.w[r] >> (4 * s - 2)) & 63u);
+            },
+            [&](uint32_t wi) { return C64{pa[wi].x, pa[wi].y, pb[wi].x, pb[wi].y}; },
             [&](const C64& m, int) { acc = c64_mul(acc, m); });
     } else if (g.full(k)) {
         const double2* pa = P2A + slot * 64;
@@ -2252,7 +2280,8 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
                            packed, g, w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount,
                            w.vhead);
     const size_t nbz = (size_t)(vc.emax - vc.emin + 1);
-    const size_t lds3x = (nbz * 16 * 2 + std::max(nbz * 64 * 2, (size_t)kW4 * 2)) * sizeof(double2);
+    const size_t lds3x = segp ? std::max((size_t)kW4 * 2, nbz * 16 * 2) * sizeof(double2)
+                              : (nbz * 16 * 2 + std::max(nbz * 64 * 2, (size_t)kW4 * 2)) * sizeof(double2);
     // K3 + K3b in one launch: the chunks' irregular blocks run as extra workgroups (segment
     // path: and block 0's walks, one lane per chunk)
     const unsigned heads3 = segp ? (unsigned)((nchunks + kThreads - 1) / kThreads) : 0u;
