@@ -288,7 +288,11 @@ constexpr int kWavesPerEU = 5;
 // kCnt: the fused training pass — each lane also counts its 64 bases' labelled transitions
 // (count_dev.h; sign = the label bits), added into the count accumulators cacc, and the last
 // workgroup finalizes both (cout: cpg_counts_i64).  Needs >= 256 lanes (chunks >= 16 Ki).
-template <bool kCnt>
+// kRep: the two-step rows (forward and backward) read from a lane-private LDS copy — key k's
+// halves at [k][lane & 15], so every ds_read_b128 lane group reads 16 distinct bank quads
+// (40 KB more LDS: 147.5 KB per workgroup); otherwise forward rows from the shared LDS rows
+// (bank conflicts) and backward rows from L1.  See launch_estep for when.
+template <bool kCnt, bool kRep>
 __global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(kWavesPerEU)))
 void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
                    unsigned long long* __restrict__ acc, const double2* __restrict__ gtab,
@@ -319,6 +323,16 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
     // the one- and two-step rows from the model's cached table (est_tables: L2-resident, 3 KB)
     // rather than per-lane reads of the kernel-argument model
     for (int i = t; i < 32 + 2 * kKeys; i += nl) TA[i] = gtab[i];   // TB, T2A, T2B follow TA
+    double2* RA = reinterpret_cast<double2*>(reinterpret_cast<unsigned char*>(fck) +
+                                             (size_t)(kLanePos / 16) * nl * sizeof(double2));
+    double2* RB = RA + kKeys * 16;
+    if (kRep)
+        for (int i = t; i < kKeys * 16; i += nl) {
+            RA[i] = gtab[32 + (i >> 4)];
+            RB[i] = gtab[32 + kKeys + (i >> 4)];
+        }
+    const double2* __restrict__ rA = RA + (t & 15);   // this lane's column of the copy
+    const double2* __restrict__ rB = RB + (t & 15);
     const Codes cd0 = lane_codes(pk, t);   // (in flight across the barrier)
     // fused counts: the workgroup's 72 count sums (LDS atomics) and the finalize's raw sums
     // in the epilogue scratch `part` (free until the epilogue's first 76 words)
@@ -569,16 +583,16 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         double2 fa[kFPD + 1], fb[kFPD + 1];
 #pragma unroll
         for (int j = 0; j < kFPD; ++j) {
-            fa[j] = T2A[key(j)];
-            fb[j] = T2B[key(j)];
+            fa[j] = kRep ? rA[key(j) * 16] : T2A[key(j)];
+            fb[j] = kRep ? rB[key(j) * 16] : T2B[key(j)];
         }
 #pragma unroll
         for (int j = 0; j < kB; ++j) {
             alP[j] = xP;
             alM[j] = xM;
             if (j + kFPD < kB) {
-                fa[(j + kFPD) % (kFPD + 1)] = T2A[key(j + kFPD)];
-                fb[(j + kFPD) % (kFPD + 1)] = T2B[key(j + kFPD)];
+                fa[(j + kFPD) % (kFPD + 1)] = kRep ? rA[key(j + kFPD) * 16] : T2A[key(j + kFPD)];
+                fb[(j + kFPD) % (kFPD + 1)] = kRep ? rB[key(j + kFPD) * 16] : T2B[key(j + kFPD)];
             }
             __builtin_amdgcn_sched_barrier(0);
             const double2 ma = fa[j % (kFPD + 1)], mb = fb[j % (kFPD + 1)];
@@ -599,8 +613,8 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
 #pragma unroll
         for (int j = 0; j < kPFD; ++j) {
             const uint32_t k = key(kB - 1 - j);
-            qa[j] = g2a[k];
-            qb[j] = g2b[k];
+            qa[j] = kRep ? rA[k * 16] : g2a[k];
+            qb[j] = kRep ? rB[k * 16] : g2b[k];
         }
 #pragma unroll
         for (int j = kB - 1; j >= 0; --j) {
@@ -608,8 +622,8 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
             // sinking them to their use (one L1/L2 round trip on every block's chain)
             if (j - kPFD >= 0) {
                 const uint32_t k = key(j - kPFD);
-                qa[(kB - 1 - j + kPFD) % (kPFD + 1)] = g2a[k];
-                qb[(kB - 1 - j + kPFD) % (kPFD + 1)] = g2b[k];
+                qa[(kB - 1 - j + kPFD) % (kPFD + 1)] = kRep ? rA[k * 16] : g2a[k];
+                qb[(kB - 1 - j + kPFD) % (kPFD + 1)] = kRep ? rB[k * 16] : g2b[k];
             }
             __builtin_amdgcn_sched_barrier(0);
             const uint32_t k = key(j);
@@ -775,10 +789,17 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
 size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep + 1024; }
 
 namespace {
-size_t estep_lds(int lanes) {   // the union is sized for 16 waves; fewer lanes use a prefix
+size_t estep_lds(int lanes, bool rep) {   // the union is sized for 16 waves; fewer lanes use a prefix
     const size_t ck = (size_t)(kLanePos / 16) * lanes * sizeof(double2);
-    return kUnionOff + kUnionBytes + 16 * 64 * sizeof(unsigned long long) + ck;
+    return kUnionOff + kUnionBytes + 16 * 64 * sizeof(unsigned long long) + ck +
+           (rep ? (size_t)kKeys * 16 * 2 * sizeof(double2) : 0);
 }
+// The lane-private row copy (kRep) makes the pass itself 7-10 % faster (46 Mbp: 0.0959 ->
+// 0.0887 ms; 3.1 Gbp: 4.89 -> 4.38 ms) but takes 40 KB of LDS from the decode kernels that
+// share the training CUs: the overlapped C2 step (702 chunks) lost 2.5 %, the C3 genome on one
+// GPU (47,303 chunks) gained 7 % (365-372 -> 395-397 Gbase/s; profiles/r04_rep/).  Used from
+// 2,048 chunks (128 Mbp) on: the multi-GPU C3 shards (5,900 chunks at 8 GPUs) and up.
+constexpr int64_t kEstRepMinChunks = 2048;
 }  // namespace
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
@@ -792,9 +813,14 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
         if (!gtab) return hipErrorInvalidValue;   // est_tables
         unsigned int* done =
             parts == PART_ALL ? reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep) : nullptr;
-        hipLaunchKernelGGL(k_estep_chunk<false>, dim3((unsigned)nchunks), dim3(lanes),
-                           estep_lds(lanes), s, model, packed, C, acc, gtab, done, out, nullptr,
-                           nullptr, nullptr);
+        if (nchunks >= kEstRepMinChunks)
+            hipLaunchKernelGGL((k_estep_chunk<false, true>), dim3((unsigned)nchunks), dim3(lanes),
+                               estep_lds(lanes, true), s, model, packed, C, acc, gtab, done, out,
+                               nullptr, nullptr, nullptr);
+        else
+            hipLaunchKernelGGL((k_estep_chunk<false, false>), dim3((unsigned)nchunks), dim3(lanes),
+                               estep_lds(lanes, false), s, model, packed, C, acc, gtab, done, out,
+                               nullptr, nullptr, nullptr);
         if (done) return hipGetLastError();
     }
     if (parts & PART_FINAL)
@@ -815,9 +841,14 @@ hipError_t launch_train(const cpg_model& model, const uint32_t* packed, const ui
     }
     const int lanes = (int)(C / kLanePos);
     unsigned int* done = reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep);
-    hipLaunchKernelGGL(k_estep_chunk<true>, dim3((unsigned)nchunks), dim3(lanes),
-                       estep_lds(lanes), s, model, packed, C, acc, gtab, done, out, sign, cacc,
-                       cout);
+    if (nchunks >= kEstRepMinChunks)
+        hipLaunchKernelGGL((k_estep_chunk<true, true>), dim3((unsigned)nchunks), dim3(lanes),
+                           estep_lds(lanes, true), s, model, packed, C, acc, gtab, done, out, sign,
+                           cacc, cout);
+    else
+        hipLaunchKernelGGL((k_estep_chunk<true, false>), dim3((unsigned)nchunks), dim3(lanes),
+                           estep_lds(lanes, false), s, model, packed, C, acc, gtab, done, out, sign,
+                           cacc, cout);
     return hipGetLastError();
 }
 
