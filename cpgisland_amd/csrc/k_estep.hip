@@ -799,7 +799,10 @@ size_t estep_lds(int lanes, bool rep) {   // the union is sized for 16 waves; fe
 // share the training CUs: the overlapped C2 step (702 chunks) lost 2.5 %, the C3 genome on one
 // GPU (47,303 chunks) gained 7 % (365-372 -> 395-397 Gbase/s; profiles/r04_rep/).  Used from
 // 2,048 chunks (128 Mbp) on: the multi-GPU C3 shards (5,900 chunks at 8 GPUs) and up.
-constexpr int64_t kEstRepMinChunks = 2048;
+#ifndef CPG_EST_REP_MIN   // (a build-time override for measurement builds only)
+#define CPG_EST_REP_MIN 2048
+#endif
+constexpr int64_t kEstRepMinChunks = CPG_EST_REP_MIN;
 }  // namespace
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
