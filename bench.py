@@ -243,6 +243,92 @@ def warm_up(step_fn, args, dist, dev):
     return done
 
 
+def launch_ranks(n, cmd=None):
+    """`bench.py --gpus N` (N > 1) started without a launcher: start N rank processes of this
+    same command line (RANK / LOCAL_RANK / WORLD_SIZE / MASTER_* set, one GPU each), before
+    this process has touched the GPU, and return the worst exit status.  Rank 0's JSON line
+    is the only stdout line (the children inherit stdout).  `cmd`: another command per rank
+    (tests/test_dist.py)."""
+    import socket
+    import subprocess
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as so_:
+        so_.bind(("127.0.0.1", 0))
+        port = so_.getsockname()[1]
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), LOCAL_RANK=str(r), WORLD_SIZE=str(n),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen(cmd or ([sys.executable, os.path.abspath(__file__)] +
+                                              sys.argv[1:]), env=env))
+    rc = 0
+    try:
+        for p in procs:
+            c = p.wait()
+            rc = rc or c
+            if c:   # one rank failed: the others would wait in a collective forever
+                for q in procs:
+                    if q.poll() is None:
+                        q.kill()
+    finally:
+        for q in procs:
+            if q.poll() is None:
+                q.kill()
+    return rc
+
+
+def sha256_hex(*arrays):
+    import hashlib
+    h = hashlib.sha256()
+    for a in arrays:
+        h.update(np.ascontiguousarray(a).view(np.uint8).tobytes())
+    return h.hexdigest()
+
+
+def bw_iteration_leg(ctx, estep_fn, decode_fn, nbases, iters, dist, dev, backend="nccl"):
+    """Real Baum-Welch iterations back to back (BaumWelchDriver.runBaumWelchMR's loop,
+    :200-203): E-step on the current model (the mapper; its per-model tables built when the
+    model is new) -> the reducer over ranks -> row normalisation on the host -> the next
+    E-step, `iters` times from the reference's initial model, then one decode (Viterbi +
+    islands) with the trained model (its per-model tables built there).  Wall time, priced
+    with every per-model cost the fixed-model headline builds before its timed region."""
+    from cpgisland_amd import HmmModel, baumwelch
+    from cpgisland_amd import dist as cdist
+    torch.cuda.synchronize()
+    if dist:
+        torch.distributed.barrier()
+    m = HmmModel.initial()
+    per, lls = [], []
+    t0 = time.perf_counter()
+    for _ in range(iters):
+        ta = time.perf_counter()
+        e = estep_fn(m)
+        if dist and backend == "nccl":
+            cdist.merge_counts_f64(e)
+            c = e.cpu().numpy()
+        elif dist:
+            c = cdist.merge_counts_f64(e.cpu()).numpy()
+        else:
+            c = e.cpu().numpy()
+        lls.append(float(c[-1]))
+        m = baumwelch.normalize(c)
+        per.append((time.perf_counter() - ta) * 1e3)
+    tb = time.perf_counter()
+    decode_fn(m)
+    torch.cuda.synchronize()
+    ctx.sync(None)
+    t1 = time.perf_counter()
+    dec_ms = (t1 - tb) * 1e3
+    return {"iterations": iters, "ms_per_iteration": round(sum(per) / iters, 4),
+            "iteration_ms": [round(x, 4) for x in per], "decode_ms": round(dec_ms, 4),
+            "total_ms": round((t1 - t0) * 1e3, 4),
+            "bases_per_s": nbases * (iters + 1) / (t1 - t0),
+            "loglik": lls,
+            "note": ("E-step -> merge -> host normalize -> next E-step (per-model tables built "
+                     "for every new model), then one decode with the trained model; bases_per_s "
+                     "counts each iteration and the decode as one pass over the bases")}
+
+
 C3_BASES = 3_100_000_000       # configs[2]: 3.1 Gbp hg38-sized genome over the node's GPUs
 C3_SEED = 20251015 + 2         # SURVEY §8(d): seed + config index
 
@@ -394,12 +480,9 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
                                    torch.cuda.Stream(), torch.cuda.Stream())
     ev = {k: [torch.cuda.Event() for _ in range(2)] for k in
           ("halo", "tr_done", "dec_done", "rec", "red", "isl")}
-    # several ranks on ONE GPU (the CPG_BENCH_BACKEND=gloo rehearsal on a one-GPU box): the
-    # decode's look-back kernels (the island resolve, K1's segment look-back) spin on flags of
-    # earlier workgroups of their own launch, which is safe for one launch but not for two
-    # processes' launches sharing the CUs — each can hold every slot spinning while the other's
-    # awaited workgroups wait for one.  The ranks then take turns for the decode (host
-    # barriers: a rehearsal of the code path, not a rate); one process per GPU never does this.
+    # several ranks on ONE GPU (the CPG_BENCH_BACKEND=gloo rehearsal on a one-GPU box): their
+    # decodes run concurrently — the island records of a shard this size are placed by the
+    # two-pass resolve (k_islands.hip: no workgroup waits for another)
     shared = bool(dist) and torch.cuda.device_count() < world
     ntr = []   # (start, end) timing events of the training pass, every 4th timed step
 
@@ -441,14 +524,8 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
             s_dec.wait_event(ev["halo"][b])
             if k >= 2:
                 s_dec.wait_event(ev["isl"][b])   # step k-2's island gather has read the records
-            for r in (range(world) if shared else (rank,)):
-                if r == rank:
-                    D.decode(ctx, model1, bp[de_o // 16:], de_n, DECODE, cap=icap,
-                             first_chunk=pl.d0, sign_out=so, score=score, out=iout[b],
-                             count=icnt[b])
-                if shared:   # ranks sharing one GPU (the gloo rehearsal) take turns
-                    s_dec.synchronize()
-                    torch.distributed.barrier()
+            D.decode(ctx, model1, bp[de_o // 16:], de_n, DECODE, cap=icap, first_chunk=pl.d0,
+                     sign_out=so, score=score, out=iout[b], count=icnt[b])
             ev["dec_done"][b].record(s_dec)
         with torch.cuda.stream(s_tr):
             s_tr.wait_event(ev["halo"][b])
@@ -500,6 +577,25 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
         [int(icnt[last].item())]
     if max(counts) > icap:
         raise RuntimeError(f"island records per rank {max(counts)} exceed the gather capacity {icap}")
+    # fingerprints of the last step's results, comparable across N (bit-exact by
+    # construction): the island records gathered on rank 0 in chunk order (rank order = chunk
+    # order, each rank's in chunk order) and the merged labelled int64 counts
+    fp = None
+    if rank == 0:
+        if world > 1:
+            recs = np.concatenate([gat_i[last][r][:counts[r]].cpu().numpy().reshape(-1)
+                                   for r in range(world)])
+        else:
+            recs = iout[last][:counts[0]].cpu().numpy().reshape(-1)
+        fp = {"records_sha256": sha256_hex(recs), "counts_sha256": sha256_hex(lmerged.cpu().numpy()),
+              "islands": int(sum(counts))}
+    bw = None
+    if args.bw_iters > 0:
+        def dec_fn(m):
+            D.decode(ctx, m, bufs[0][0][de_o // 16:], de_n, DECODE, cap=icap, first_chunk=pl.d0,
+                     sign_out=so, score=score, out=iout[0], count=icnt[0])
+        bw = bw_iteration_leg(ctx, lambda m: D.bw_estep(ctx, m, bufs[0][0][tr_o // 16:], tr_n, TRAIN),
+                              dec_fn, G, args.bw_iters, dist, dev, backend)
     if rank == 0:
         ms = elapsed * 1e3 / args.steps
         value = G * args.steps / elapsed
@@ -532,7 +628,8 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
                "cpu_baseline": None,
                "cpu_baseline_note": ("the CPU baseline is measured on rank 0 at N = 1 only (the "
                                      "bench contract): the n_gpus = 1 line's cpu_baseline, the "
-                                     "oracle on a bounded sample of the same synthetic genome")}
+                                     "oracle on a bounded sample of the same synthetic genome"),
+               "fingerprint": fp, "bw_iteration": bw}
         # HBM traffic of the training pass at this rank's size: the PMC profile of the C3
         # workload on one GPU (tools/pmc.sh c3), scaled to the shard's bases
         pmc = _pmc_traffic(ESTEP_KERNEL, tr_n, name="pmc_c3.json", scale=True)
@@ -589,6 +686,10 @@ def main():
     ap.add_argument("--separate-train", action="store_true",
                     help="E-step and labelled counts as two launches instead of the fused "
                          "training pass (cpg_train_pass_d)")
+    ap.add_argument("--bw-iters", type=int, default=5,
+                    help="after the timed steps: this many real Baum-Welch iterations back to back "
+                         "(new model every iteration) + one decode, reported as bw_iteration (0 = "
+                         "skip)")
     ap.add_argument("--cpu-sample", type=int, default=192 * DECODE)
     ap.add_argument("--cpu-threads", type=int, default=16,
                     help="host threads for the CPU baseline (the GPU box's CPU share is 16)")
@@ -647,6 +748,10 @@ def main():
     args = ap.parse_args()
     if args.flush_mb:
         args.serial = True   # the flushed step time is the sum of isolated phase times
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        sys.exit(launch_ranks(args.gpus))     # one process per GPU, started here
+    if int(os.environ.get("WORLD_SIZE", "1")) != args.gpus:
+        sys.exit(f"bench.py: WORLD_SIZE={os.environ.get('WORLD_SIZE')} but --gpus {args.gpus}")
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -967,6 +1072,15 @@ def main():
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
         elapsed = float(t.item())
+    islands_found = int(lanes[0]["icnt"].item()) + sum(int(p["icnt"].item()) for p in lanes[0]["parts"])
+    bw = None
+    if args.bw_iters > 0:
+        ln0 = lanes[0]
+        bw = bw_iteration_leg(
+            ctx, lambda m: D.bw_estep(ctx, m, dp, N, TRAIN, out=ln0["ecnt"]),
+            lambda m: decode_step(ctx, m, dp, N, ln0["so"], ln0["score"], ln0["iout"], ln0["icnt"],
+                                  fused_decode, first_chunk),
+            N * world, args.bw_iters, dist, dev, backend)
     cold = None
     if args.cold_steps > 0 and not dist and not args.flush_mb:
         cold = cold_cache_steps(lanes[0], dp, ds, N, model0, model1, args.cold_steps, main_s, dev,
@@ -982,7 +1096,8 @@ def main():
         if c3_leg is not None:
             c3_leg = {k: c3_leg[k] for k in ("value", "unit", "ms_per_step", "steps",
                                               "warmup_steps_run", "scaling", "config",
-                                              "phases_ms", "roofline", "roofline_count")
+                                              "phases_ms", "roofline", "roofline_count",
+                                              "fingerprint", "bw_iteration")
                       if k in c3_leg}
     steps = args.steps
     ms_per_step = elapsed * 1e3 / steps
@@ -1066,12 +1181,12 @@ def main():
                                          "built before the timed region"),
                           "collectives": (("rccl" if backend == "nccl" else backend)
                                           if dist else None),
-                          "islands_found": int(lanes[0]["icnt"].item()) +
-                                           sum(int(p["icnt"].item()) for p in lanes[0]["parts"])},
+                          "islands_found": islands_found},
                "phases_ms": {k: round(v, 4) for k, v in phases.items()},
                "host_issue_ms_per_step": round(issue * 1e3 / steps, 4),
                "roofline": roof, "roofline_fp64": roof_fp64, "roofline_decode": roof_decode,
-               "roofline_decode_valu": roof_decode_valu, "cold_cache": cold}
+               "roofline_decode_valu": roof_decode_valu, "cold_cache": cold,
+               "bw_iteration": bw}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(SEED, args.cpu_sample,
                                                 min(args.cpu_threads, os.cpu_count() or 1))

@@ -12,7 +12,7 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.environ.get("CPG_LIB_OVERRIDE") or os.path.join(_HERE, "libcpg.so")  # override: dev ablations only
+LIB_PATH = os.path.join(_HERE, "libcpg.so")   # the in-tree build, nothing else
 
 CPG_OK = 0
 CPG_E_INVALID = -1
@@ -94,6 +94,13 @@ SIGNATURES = {
     "cpg_contigs_islands_d": [_P, _P, _P, _I64, _P, _P, _P, _I64, _P, _I64, _P, _P],
 }
 
+# test hooks exported by libcpg.so outside the C-ABI (cpg_internal.h): the readers started
+# from a given Java `count` (the 2^32 wrap with a few MB of text; tests only)
+TEST_HOOKS = {
+    "cpgx_ingest_at": [C.c_char_p, C.c_size_t, _INT, _INT, _P, _I64, _P, C.c_uint32],
+    "cpgx_ingest_gpu_at": [_P, C.c_char_p, C.c_size_t, _INT, _INT, _P, _I64, _P, C.c_uint32],
+}
+
 
 def _load():
     if not os.path.exists(LIB_PATH):
@@ -112,7 +119,7 @@ def _load():
     except ImportError:
         pass
     lib = C.CDLL(LIB_PATH)
-    for name, args in SIGNATURES.items():
+    for name, args in {**SIGNATURES, **TEST_HOOKS}.items():
         fn = getattr(lib, name)
         fn.argtypes = args
         fn.restype = _INT

@@ -597,13 +597,15 @@ int cpg_merge_train_d(cpg_ctx* ctx, const void* d_gathered, int world, double* d
     return CPG_OK;
 }
 
-int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compat_quirks,
-                 uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result,
-                 void* stream) {
+static int ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compat_quirks,
+             uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result, void* stream,
+             uint32_t count0) {
     if (!ctx || !d_result || (n > 0 && !d_txt) || (cap_bases > 0 && !d_packed))
         return set_error(CPG_E_INVALID, "cpg_ingest_d: null argument");
     if (n < 0 || cap_bases < 0 || (mode != 0 && mode != 1))
         return set_error(CPG_E_INVALID, "cpg_ingest_d: bad argument");
+    const int64_t chunk = mode == 0 ? CPG_TRAIN_CHUNK : CPG_DECODE_CHUNK;
+    if (count0 % chunk) return set_error(CPG_E_INVALID, "ingest: count0 not a chunk multiple");
     if (!aligned16(d_txt) || !aligned16(d_packed))
         return set_error(CPG_E_INVALID, "cpg_ingest_d: buffers must be 16-byte aligned");
     std::lock_guard<std::mutex> lk(ctx->mu);
@@ -611,11 +613,17 @@ int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compa
     void* ws;
     int rc;
     if ((rc = ws_get(ctx, WS_ING, ingest_ws_bytes(n), &ws))) return rc;
-    CPG_HIP(launch_ingest(reinterpret_cast<const uint8_t*>(d_txt), n, mode, compat_quirks,
-                          mode == 0 ? CPG_TRAIN_CHUNK : CPG_DECODE_CHUNK, d_packed, cap_bases,
-                          ws, ctx->ws[WS_ING].bytes, reinterpret_cast<long long*>(d_result),
-                          pick(ctx, stream)));
+    CPG_HIP(launch_ingest(reinterpret_cast<const uint8_t*>(d_txt), n, mode, compat_quirks, chunk,
+                          d_packed, cap_bases, ws, ctx->ws[WS_ING].bytes,
+                          reinterpret_cast<long long*>(d_result), pick(ctx, stream), count0));
     return CPG_OK;
+}
+
+int cpg_ingest_d(cpg_ctx* ctx, const char* d_txt, int64_t n, int mode, int compat_quirks,
+                 uint32_t* d_packed, int64_t cap_bases, cpg_ingest_result* d_result,
+                 void* stream) {
+    return ingest_d(ctx, d_txt, n, mode, compat_quirks, d_packed, cap_bases, d_result, stream,
+                    0u);
 }
 
 // ---- host-buffer entry points -------------------------------------------------------
@@ -730,8 +738,8 @@ int cpg_decode_states(cpg_ctx* ctx, const cpg_model* model, const int32_t* obs, 
     return CPG_OK;
 }
 
-int cpg_ingest_gpu(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat_quirks,
-                   uint32_t* packed, int64_t cap_bases, int64_t* nbases) {
+static int ingest_gpu(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat_quirks,
+                      uint32_t* packed, int64_t cap_bases, int64_t* nbases, uint32_t count0) {
     if (!ctx || !nbases || (n > 0 && !txt) || (cap_bases > 0 && !packed) || cap_bases < 0 ||
         (mode != 0 && mode != 1))
         return set_error(CPG_E_INVALID, "cpg_ingest_gpu: bad argument");
@@ -744,8 +752,8 @@ int cpg_ingest_gpu(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat
         CPG_TRY(ws_get(ctx, WS_OUT0, (size_t)((cap_bases + 15) / 16) * 4 + 16, &dp));
         CPG_TRY(ws_get(ctx, WS_OUT1, sizeof(cpg_ingest_result), &dr));
     }
-    CPG_TRY(cpg_ingest_d(ctx, (const char*)dt, (int64_t)n, mode, compat_quirks, (uint32_t*)dp,
-                         cap_bases, (cpg_ingest_result*)dr, ctx->stream));
+    CPG_TRY(ingest_d(ctx, (const char*)dt, (int64_t)n, mode, compat_quirks, (uint32_t*)dp,
+                     cap_bases, (cpg_ingest_result*)dr, ctx->stream, count0));
     cpg_ingest_result r;
     CPG_HIP(hipMemcpyAsync(&r, dr, sizeof r, hipMemcpyDeviceToHost, ctx->stream));
     CPG_TRY(cpg_sync(ctx, ctx->stream));
@@ -757,13 +765,24 @@ int cpg_ingest_gpu(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat
     if (r.status == CPG_E_REF_CRASH)
         return set_error(CPG_E_REF_CRASH,
                          "reference throws at input byte %lld (decode reader on an empty list, "
-                         "or the base count wrapped past 2^32)", (long long)r.crash_byte);
+                         "or the training reader's chunk vector past a 2^32 count wrap)", (long long)r.crash_byte);
     if (r.status == CPG_E_CAPACITY)
         return set_error(CPG_E_CAPACITY, "cpg_ingest_gpu: capacity %lld bases exceeded",
                          (long long)cap_bases);
     if (r.status != CPG_OK)
         return set_error((int)r.status, "cpg_ingest_gpu: device look-back timed out");
     return CPG_OK;
+}
+
+int cpg_ingest_gpu(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat_quirks,
+                   uint32_t* packed, int64_t cap_bases, int64_t* nbases) {
+    return ingest_gpu(ctx, txt, n, mode, compat_quirks, packed, cap_bases, nbases, 0u);
+}
+
+// test hook (cpg_internal.h): the device reader from Java count = count0
+int cpgx_ingest_gpu_at(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat_quirks,
+                       uint32_t* packed, int64_t cap_bases, int64_t* nbases, uint32_t count0) {
+    return ingest_gpu(ctx, txt, n, mode, compat_quirks, packed, cap_bases, nbases, count0);
 }
 
 int cpg_islands(cpg_ctx* ctx, const uint32_t* packed, const uint32_t* sign, int64_t nbases,

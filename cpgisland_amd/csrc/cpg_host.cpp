@@ -167,14 +167,22 @@ int cpg_initial_model(cpg_model* m) {
     return CPG_OK;
 }
 
-// CpGIslandFinder.java:112-145 (mode 0) and :238-259 (mode 1).
-int cpg_ingest(const char* txt, size_t n, int mode, int compat_quirks, uint32_t* packed,
-               int64_t cap_bases, int64_t* nbases) {
+// CpGIslandFinder.java:112-145 (mode 0) and :238-259 (mode 1), from Java `count` = count0
+// with an empty list (cpg_ingest: 0; the test hook cpgx_ingest_at: a multiple of the chunk).
+// `count` is a Java int: at 2^32 bases it wraps to 0 and the chunk test is skipped, so the
+// list keeps its chunk and grows by another chunk until the next multiple.  There the
+// training reader's DenseVector(0x10000).set(0x10000, …) throws (:133-134: a crash at the
+// valid byte that brings count to 2^32 + 65,536), while the decode reader copies get(0 ..
+// 2^20-1) — the held chunk — and clear() silently drops the 2^20 bases read after the wrap
+// (:257-259); a non-ACGT byte read while count == 0 fires nothing.
+static int ingest_host(const char* txt, size_t n, int mode, int compat_quirks, uint32_t* packed,
+                       int64_t cap_bases, int64_t* nbases, uint32_t count0) {
     if (!txt || !packed || !nbases || (mode != 0 && mode != 1) || cap_bases < 0)
         return set_error(CPG_E_INVALID, "cpg_ingest: bad argument");
     const uint32_t mask = mode == 0 ? 0xFFFFu : 0xFFFFFu;
     const int64_t chunk = mode == 0 ? CPG_TRAIN_CHUNK : CPG_DECODE_CHUNK;
-    uint32_t count = 0;          // Java int count (wraps)
+    if (count0 & mask) return set_error(CPG_E_INVALID, "ingest: count0 not a chunk multiple");
+    uint32_t count = count0;     // Java int count (wraps)
     int64_t listlen = 0;         // bases pending in observedSequence
     int64_t out = 0;             // bases committed (whole chunks)
     *nbases = 0;
@@ -187,18 +195,22 @@ int cpg_ingest(const char* txt, size_t n, int mode, int compat_quirks, uint32_t*
     for (size_t k = 0; k < n; ++k) {
         int v = sym_of((unsigned char)txt[k]);
         if (v != -1) {
-            if (listlen >= chunk) {
-                *nbases = out;
-                return set_error(CPG_E_REF_CRASH,
-                                 "base count wrapped past 2^32 (Java int): the reference "
-                                 "would overflow its chunk vector");
-            }
-            if (out + listlen < cap_bases) put(out + listlen, v);   // tail may not fit
+            // past a wrap the decode reader's bases beyond the held chunk are dropped at the
+            // next multiple (or stay an undecoded tail): not written
+            if (out + listlen < cap_bases && (mode == 0 || listlen < chunk))
+                put(out + listlen, v);
             listlen++;
             count++;
         }
         if (count != 0 && (count & mask) == 0) {
-            if (listlen == chunk) {
+            if (listlen > chunk && mode == 0) {
+                *nbases = out;
+                return set_error(CPG_E_REF_CRASH,
+                                 "reference throws IndexOutOfBoundsException at input byte "
+                                 "%zu (:133-134: the base count wrapped past 2^32, the chunk "
+                                 "vector gets %lld bases)", k, (long long)listlen);
+            }
+            if (listlen >= chunk) {      // == chunk, or 2 chunks after a wrap (mode 1)
                 if (out + chunk > cap_bases) {
                     *nbases = out;
                     return set_error(CPG_E_CAPACITY, "cpg_ingest: capacity %lld bases exceeded",
@@ -224,6 +236,17 @@ int cpg_ingest(const char* txt, size_t n, int mode, int compat_quirks, uint32_t*
     }
     *nbases = out;          // tail (listlen bases) is never processed by the reference
     return CPG_OK;
+}
+
+int cpg_ingest(const char* txt, size_t n, int mode, int compat_quirks, uint32_t* packed,
+               int64_t cap_bases, int64_t* nbases) {
+    return ingest_host(txt, n, mode, compat_quirks, packed, cap_bases, nbases, 0u);
+}
+
+// test hook (cpg_internal.h, not part of cpg.h): the reader from Java count = count0
+int cpgx_ingest_at(const char* txt, size_t n, int mode, int compat_quirks, uint32_t* packed,
+                   int64_t cap_bases, int64_t* nbases, uint32_t count0) {
+    return ingest_host(txt, n, mode, compat_quirks, packed, cap_bases, nbases, count0);
 }
 
 // ---------------------------------------------------------------------------------

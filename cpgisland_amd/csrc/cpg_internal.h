@@ -274,9 +274,21 @@ hipError_t launch_contigs_islands(const uint32_t* packed, const uint32_t* sign, 
                                   int64_t n, void* ws, size_t ws_bytes, cpg_island* out,
                                   int64_t cap, int64_t* count, uint32_t* status, hipStream_t s);
 
+// count0: the Java `count` before the first byte (0; the test hooks below: a chunk multiple)
 hipError_t launch_ingest(const uint8_t* txt, int64_t n, int mode, int quirks, int64_t chunk,
                          uint32_t* out, int64_t cap, void* ws, size_t ws_bytes,
-                         long long* res, hipStream_t s);
+                         long long* res, hipStream_t s, uint32_t count0 = 0);
 size_t ingest_ws_bytes(int64_t n);
 
 }  // namespace cpg
+
+// Test hooks, exported but not part of the C-ABI (include/cpg.h): the readers of cpg_ingest /
+// cpg_ingest_gpu started from Java `count` = count0 (a multiple of the chunk below 2^32) with
+// an empty list, so that the int counter's wrap at 2^32 bases (:127, :253) is reached with a
+// few MB of text (tests/test_ingest_wrap.py, tests/test_gpu_ingest.py).
+extern "C" {
+int cpgx_ingest_at(const char* txt, size_t n, int mode, int compat_quirks, uint32_t* packed,
+                   int64_t cap_bases, int64_t* nbases, uint32_t count0);
+int cpgx_ingest_gpu_at(cpg_ctx* ctx, const char* txt, size_t n, int mode, int compat_quirks,
+                       uint32_t* packed, int64_t cap_bases, int64_t* nbases, uint32_t count0);
+}

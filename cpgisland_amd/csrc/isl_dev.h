@@ -112,6 +112,10 @@ struct IslWs {
     Cnt5* toff;         // per tile: exclusive prefix in its chunk (kernel R)
     int32_t* kept;      // per chunk, maxr: rank*2 | stale_in, or -1
     unsigned long long* flags;   // per chunk: epoch << 32 | kept islands (look-back)
+    // the two-pass resolve (separate island kernels: no look-back): per chunk {kept islands,
+    // closed runs}, per chunk and lane {keep/map bits, stale_in | local rank << 1}
+    int2* cres;
+    uint2* lanest;
     int64_t ntile;      // tiles per chunk
     int64_t cap_t;      // records per tile and kind
     size_t bytes;
@@ -355,7 +359,10 @@ __device__ __forceinline__ long long kept_before(const IslWs& ws, int64_t c, uin
 // filtered (:280-285), kept islands ranked, the chunk's first record found by the look-back,
 // records written.  With <= 8 runs per lane the map and both filter outcomes (stale 0 / 1)
 // of each run stay in registers: one pass of loads before the records.
-template <bool kAgent, bool kAgentRec>
+// kSplit (the separate kernels' first pass, no look-back): the chunk's kept count and run
+// count go to ws.cres, each lane's cached bits, stale_in and rank to ws.lanest, and
+// write_runs (second pass) places the records once every chunk's count is known.
+template <bool kAgent, bool kAgentRec, bool kSplit = false>
 __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws, const Cnt5* to,
                                              int64_t c, int64_t C, int64_t nr, int32_t* kept,
                                              uint32_t* sm, int32_t* sk, long long* sbase,
@@ -397,12 +404,20 @@ __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws
     }
     int32_t nkt;
     int32_t rank = wg_scan_sum(nk, sk, nkt);
+    if constexpr (kSplit) {
+        ws.lanest[c * nl + t] = make_uint2(bits, stale0 | ((uint32_t)rank << 1));
+        if (t == 0) ws.cres[c] = make_int2(nkt, (int32_t)nr);
+        return;
+    }
     // publish this chunk's count, then find the kept islands of the chunks before it
     if (t == 0)
         __hip_atomic_store(ws.flags + c, ((unsigned long long)o.epoch << 32) | (uint32_t)nkt,
                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     if (t < 64) {
         const long long before = kept_before(ws, c, o.epoch, o.status);
+        // the flag word holds 31 bits of prefix: a call with 2^31 islands or more cannot be
+        // placed — report it as a failed look-back instead of wrapping silently
+        if (t == 0 && before + nkt >= (long long)kInclusive) atomicOr(o.status, ST_LOOKBACK_TIMEOUT);
         if (t == 0) {
             *sbase = before;
             __hip_atomic_store(ws.flags + c,
@@ -473,14 +488,14 @@ struct ResolveLds {
 // decode): tile offsets (exclusive scan of the chunk's tile totals in blocks of blockDim.x
 // tiles; in LDS `s_to` for up to kToff tiles, else in ws.toff), then resolve_runs.
 // kAgentRec: the tile lists and totals were written by other workgroups of this kernel.
-template <bool kAgentRec, int kToff>
+template <bool kAgentRec, int kToff, bool kSplit = false>
 __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C, const IslWs& ws,
                                               const IslOut& o, int64_t c, ResolveLds& L,
                                               Cnt5* s_to) {
     const int t = threadIdx.x, nl = blockDim.x;
     const int64_t maxr = C / 2 + 1;
     const uint32_t* pk = packed + c * (C / 16);
-    const bool in_lds = ws.ntile <= kToff;
+    const bool in_lds = !kSplit && ws.ntile <= kToff;   // kSplit: write_runs reads ws.toff
     Cnt5 carry{0, 0, 0, 0, 0};
     for (int64_t b = 0, it = 0; b < ws.ntile; b += nl, ++it) {
         const int64_t i = b + t;
@@ -501,10 +516,56 @@ __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C,
     const int64_t nr = carry.cl;
     int32_t* kept = ws.kept + c * maxr;
     if (in_lds)
-        resolve_runs<false, kAgentRec>(pk, ws, s_to, c, C, nr, kept, L.sm, L.sk, &L.sbase, o);
+        resolve_runs<false, kAgentRec, kSplit>(pk, ws, s_to, c, C, nr, kept, L.sm, L.sk, &L.sbase, o);
     else
-        resolve_runs<true, kAgentRec>(pk, ws, ws.toff + c * ws.ntile, c, C, nr, kept, L.sm, L.sk,
-                                      &L.sbase, o);
+        resolve_runs<true, kAgentRec, kSplit>(pk, ws, ws.toff + c * ws.ntile, c, C, nr, kept, L.sm,
+                                              L.sk, &L.sbase, o);
+}
+
+// The second pass of the two-pass resolve: chunk c's first record = the kept islands of the
+// chunks before it (a workgroup sum over ws.cres, written by the first pass — an earlier
+// kernel, so no workgroup waits for another), then every lane writes its kept islands from
+// the bits and rank the first pass left (run stats re-read for the kept runs only).
+__device__ __forceinline__ void write_runs(const uint32_t* packed, int64_t C, const IslWs& ws,
+                                           const IslOut& o, int64_t c, long long* s_part) {
+    const int t = threadIdx.x, nl = blockDim.x, lane = t & 63, wv = t >> 6;
+    long long before = 0;
+    for (int64_t j = t; j < c; j += nl) before += ws.cres[j].x;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) before += __shfl_xor(before, off);
+    if (lane == 0) s_part[wv] = before;
+    __syncthreads();
+    long long base = 0;
+    for (int w = 0; w < (nl >> 6); ++w) base += s_part[w];
+    base += o.base_in ? *o.base_in : 0;
+    const int2 cr = ws.cres[c];
+    if (c == o.nchunks - 1 && t == 0) *o.count = base + cr.x;
+    if (cr.x == 0) return;
+    const int64_t nr = cr.y;
+    const int64_t per = (nr + nl - 1) / nl;
+    const int64_t r0 = min((int64_t)t * per, nr), r1 = min(r0 + per, nr);
+    const uint2 st = ws.lanest[c * nl + t];
+    const uint32_t* pk = packed + c * (C / 16);
+    const Cnt5* to = ws.toff + c * ws.ntile;
+    const int64_t gchunk = o.first_chunk + c;
+    const uint32_t cbase = (uint32_t)gchunk * (uint32_t)C;   // chunk*0x100000, Java int
+    int64_t dst = base + (int64_t)(st.y >> 1);
+    if (per <= 8) {
+        uint32_t stale = st.y & 1u;
+        for (int64_t j = 0; j < r1 - r0; ++j) {
+            const uint32_t b = st.x >> (4 * j);
+            if ((b >> (2 + stale)) & 1u)
+                put_island(o, run_stat<false, false>(pk, ws, to, c, r0 + j), stale, dst++, gchunk,
+                           cbase);
+            stale = mapply(b & 3u, stale);
+        }
+    } else {
+        const int32_t* kept = ws.kept + c * (C / 2 + 1);
+        for (int64_t r = r0; r < r1; ++r)
+            if (kept[r] >= 0)
+                put_island(o, run_stat<false, false>(pk, ws, to, c, r), (uint32_t)(kept[r] & 1),
+                           dst++, gchunk, cbase);
+    }
 }
 
 }  // namespace isl

@@ -27,6 +27,11 @@
 //     stores, the partial words at run edges integer atomicOr into the zeroed output.
 // The look-back descriptors are 8-byte {flag, value} granules stored and polled with
 // agent-scope relaxed atomics (the data is the flag); every spin is bounded.
+// `count` is a Java int (:107, :236): at 2^32 bases it wraps to 0 and the test is skipped, so
+// the list keeps its chunk.  At the next multiple the training reader's chunk vector gets two
+// chunks (DenseVector.set(0x10000) throws at :134: a crash at that valid byte), the decode
+// reader decodes the held chunk and clear() drops the 2^20 bases read after the wrap (a
+// dropped window: the tile's bases are written as two runs around it, later bases shifted).
 // Algorithmic bytes: 1 B/byte read + 0.25 B/base written.
 
 #include "cpg_internal.h"
@@ -140,6 +145,15 @@ __device__ __forceinline__ void classify(uint4 q, uint32_t& vmask, uint32_t& cod
     }
 }
 
+// chunks committed by the firings at the multiples of C in (c0, G] (G, c0: unwrapped counts):
+// every multiple fires except the wraps k 2^32 (count == 0), and each firing commits one chunk
+// (past a wrap, the held one)
+__device__ __forceinline__ long long commits(unsigned long long G, unsigned long long c0,
+                                             long long C) {
+    return (long long)(G / (unsigned long long)C) - (long long)(G >> 32) -
+           ((long long)(c0 / (unsigned long long)C) - (long long)(c0 >> 32));
+}
+
 struct IngestArgs {
     const uint8_t* txt;
     int64_t n;
@@ -149,6 +163,7 @@ struct IngestArgs {
     int mode;           // 0 training, 1 decode
     int quirks;
     uint32_t* out;
+    unsigned long long c0;   // Java count before the first byte (a chunk multiple < 2^32)
 };
 
 __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
@@ -265,8 +280,8 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
     const unsigned long long vex = s_vex;
     const long long C = a.chunk;
     // residue point: local index l* with (vex + l*) % chunk == 0, l* <= agg
-    const long long ls = (C - (long long)(vex % (unsigned long long)C)) % C;
-    const unsigned long long gq = vex + (unsigned long long)ls;   // count at the quirk bytes
+    const long long ls = (C - (long long)(vex % (unsigned long long)C)) % C;   // c0 % C == 0
+    const unsigned long long gq = a.c0 + vex + (unsigned long long)ls;   // count at the quirk bytes
     const bool qlive = a.quirks && ls <= (long long)agg && gq != 0 && (gq % kWrap) != 0;
     if (qlive) {
 #pragma unroll
@@ -293,17 +308,19 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
             }
         }
     }
-    // the Java int count wraps to 0 at 2^32 bases: that chunk is never committed and the
-    // next base overflows the reference's chunk buffer (crash at the valid byte whose count
-    // before it is 2^32)
-    if (vex <= kWrap && vex + agg > kWrap) {
-        const uint32_t jw = (uint32_t)(kWrap - vex);
+    // the training reader's crash past a count wrap: the valid byte that brings the count to
+    // W + chunk (W = 2^32, the first wrap after c0: the stream ends there)
+    if (a.mode == 0) {
+        const unsigned long long jc = kWrap + (unsigned long long)C - 1ull - a.c0;  // its index
+        if (vex <= jc && jc < vex + agg) {
+            const uint32_t jw = (uint32_t)(jc - vex);
 #pragma unroll
-        for (int r = 0; r < kIRows; ++r) {
-            if (jw < o[r] || jw >= o[r] + cnt[r]) continue;
-            uint32_t m = vm[r];
-            for (uint32_t s = o[r]; s < jw; ++s) m &= m - 1;   // drop lower valid bytes
-            s_wrapk = base + wv * (kIRows * 1024) + r * 1024 + lane * 16 + (__builtin_ffs(m) - 1);
+            for (int r = 0; r < kIRows; ++r) {
+                if (jw < o[r] || jw >= o[r] + cnt[r]) continue;
+                uint32_t m = vm[r];
+                for (uint32_t s = o[r]; s < jw; ++s) m &= m - 1;   // drop lower valid bytes
+                s_wrapk = base + wv * (kIRows * 1024) + r * 1024 + lane * 16 + (__builtin_ffs(m) - 1);
+            }
         }
     }
     __syncthreads();
@@ -333,12 +350,11 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
         long long ck = -1, cc = 0;
         if (a.mode == 1 && qt > 0) {
             ck = s_qmin;
-            cc = (long long)gq;   // gq / chunk whole chunks committed before it
+            cc = commits(gq, a.c0, C) * C;   // the chunks committed before it
         }
         if (s_wrapk >= 0 && (ck < 0 || s_wrapk < ck)) {
             ck = s_wrapk;
-            cc = (long long)((kWrap / (unsigned long long)C - 1 + (qchain ? qp : 0)) *
-                             (unsigned long long)C);
+            cc = (commits(kWrap, a.c0, C) + (long long)(qchain ? qp : 0)) * C;
         }
         if (ck >= 0) {
             ws.crash_k[tile] = ck;
@@ -351,16 +367,37 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
             ws.tot[1] = (long long)(qp + (qchain ? (unsigned)qt : 0u));
         }
     }
-    // write the tile's bases: run A = local [0, min(agg, ls)) at P, run B = local [ls, agg)
-    // at P + ls + qt * chunk (only with a quirk gap inside this tile)
+    // write the tile's bases as two runs (local start, length, output position): with a quirk
+    // gap (training reader) run A = local [0, min(agg, ls)) at P, run B = local [ls, agg) at
+    // P + ls + qt * chunk; past a count wrap (decode reader) the bases of the dropped window
+    // (count in (W, W + chunk], W = k 2^32) are skipped and every later base moves down a chunk
     const long long P = (long long)vex + (long long)qp * C;
-    const bool gap = qchain && qt > 0;
-    const long long lenA = gap ? (ls < (long long)agg ? ls : (long long)agg) : (long long)agg;
+    long long sA = 0, lenA = (long long)agg, gA = P, sB = 0, lenB = 0, gB = 0;
+    if (qchain && qt > 0) {
+        lenA = ls < (long long)agg ? ls : (long long)agg;
+        sB = lenA;
+        lenB = (long long)agg - lenA;
+        gB = P + ls + (long long)qt * C;
+    } else if (a.mode == 1) {
+        // base l of the tile (global valid index vex + l) is dropped iff v0 + l lies in
+        // [W_k, W_k + C) for some W_k = k 2^32, k >= 1; `done` windows end at or before v0
+        const long long v0 = (long long)(a.c0 + vex);          // count before the tile
+        const long long done = v0 >= C ? (long long)((unsigned long long)(v0 - C) >> 32) : 0;
+        const long long W = (done + 1) << 32;                  // the next window's start
+        const long long wa = W - v0, wb = wa + C;              // its local range [wa, wb)
+        const long long a0 = wa < 0 ? 0 : (wa < (long long)agg ? wa : (long long)agg);
+        const long long b0 = wb < (long long)agg ? wb : (long long)agg;   // wb > 0
+        lenA = a0;
+        gA = (long long)vex - done * C;
+        sB = b0;
+        lenB = (long long)agg - b0;
+        gB = (long long)vex + b0 - (done + 1) * C;
+    }
     for (int run = 0; run < 2; ++run) {
-        const long long s0 = run == 0 ? 0 : lenA;
-        const long long len = run == 0 ? lenA : (gap ? (long long)agg - lenA : 0);
+        const long long s0 = run == 0 ? sA : sB;
+        const long long len = run == 0 ? lenA : lenB;
         if (len <= 0) continue;
-        const long long g0 = run == 0 ? P : P + ls + (long long)qt * C;
+        const long long g0 = run == 0 ? gA : gB;
         const long long gend = g0 + len < a.cap ? g0 + len : a.cap;
         if (gend <= g0) continue;
         const long long w0 = g0 >> 4, w1 = (gend - 1) >> 4;
@@ -386,12 +423,10 @@ __global__ __launch_bounds__(kIT) void k_ingest(IngestArgs a, IngestWs ws) {
 
 // One thread: totals + crash info -> the cpg_ingest_result fields (host rules of cpg_ingest)
 __global__ void k_ingest_final(IngestWs ws, int64_t chunk, int64_t cap, int mode, int quirks,
-                               long long* __restrict__ res) {
+                               unsigned long long c0, long long* __restrict__ res) {
     if (threadIdx.x != 0) return;
     const long long V = ws.tot[0], Q = ws.tot[1], C = chunk;
-    long long commits = V / C;
-    if ((unsigned long long)V >= kWrap) commits -= 1;   // count == 0 at 2^32: not committed
-    long long committed = (commits + Q) * C;
+    long long committed = (commits(c0 + (unsigned long long)V, c0, C) + Q) * C;
     long long status = CPG_OK, crash_byte = -1;
     const unsigned ct = *ws.crash_tile;
     if (ct != 0xFFFFFFFFu) {
@@ -426,7 +461,7 @@ size_t ingest_ws_bytes(int64_t n) {
 
 hipError_t launch_ingest(const uint8_t* txt, int64_t n, int mode, int quirks, int64_t chunk,
                          uint32_t* out, int64_t cap, void* wsp, size_t ws_bytes,
-                         long long* res, hipStream_t s) {
+                         long long* res, hipStream_t s, uint32_t count0) {
     const int64_t nt = (n + kTileBytes - 1) / kTileBytes;
     if (ws_bytes < ingest_ws_bytes(n) || nt >= (1ll << 31)) return hipErrorInvalidValue;
     char* w = static_cast<char*>(wsp);
@@ -446,11 +481,11 @@ hipError_t launch_ingest(const uint8_t* txt, int64_t n, int mode, int quirks, in
     if (cap > 0 && (e = hipMemsetAsync(out, 0, (size_t)((cap + 15) / 16) * 4, s)) != hipSuccess)
         return e;
     if (nt > 0) {
-        IngestArgs a{txt, n, chunk, cap, nt, mode, quirks, out};
+        IngestArgs a{txt, n, chunk, cap, nt, mode, quirks, out, (unsigned long long)count0};
         hipLaunchKernelGGL(k_ingest, dim3((unsigned)nt), dim3(kIT), 0, s, a, ws);
     }
     hipLaunchKernelGGL(k_ingest_final, dim3(1), dim3(64), 0, s, ws, chunk, cap, mode, quirks,
-                       res);
+                       (unsigned long long)count0, res);
     return hipGetLastError();
 }
 

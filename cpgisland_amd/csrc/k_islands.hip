@@ -18,8 +18,12 @@
 //     scan, and a record per run boundary with the tile-local prefix counts at it, written
 //     at its tile-local rank into the tile's slice of the run lists; the tile totals;
 //   R (per chunk): tile offsets (scan of the tile totals), per-run stats, stale-atC scan,
-//     filter, kept rank, the chunk's first record from a look-back over the earlier chunks'
-//     published counts, island records.
+//     filter, kept ranks, the chunk's kept count;
+//   W (per chunk): the chunk's first record = the kept counts of the chunks before it (summed
+//     from R's per-chunk counts: a kernel boundary instead of a look-back, so no workgroup
+//     ever waits for another), island records.
+// (The fused decode, k_viterbi.hip, resolves a chunk in its last traceback workgroup and finds
+// the chunk's first record by a decoupled look-back over the earlier chunks' flags.)
 // A whole chunk per workgroup would stream at one CU's share of the memory system (≈25-70
 // GB/s per CU): the tiles spread the one pass over the data on every CU.
 
@@ -61,7 +65,9 @@ IslWs carve_isl(void* base, int64_t nchunks, int64_t C, int64_t tw) {
     w.ttot = (Cnt5*)take(nt * sizeof(Cnt5));
     w.toff = (Cnt5*)take(nt * sizeof(Cnt5));
     w.kept = (int32_t*)take(nchunks * maxr * 4);
-    w.flags = nullptr;   // WS_IFLG (launch_islands)
+    w.cres = (int2*)take(nchunks * sizeof(int2));
+    w.lanest = (uint2*)take(nchunks * kIT * sizeof(uint2));
+    w.flags = nullptr;   // WS_IFLG (the fused decode's look-back)
     w.bytes = o + 256;
     return w;
 }
@@ -169,13 +175,19 @@ __global__ __launch_bounds__(kTT) void k_isl_tile(const uint32_t* packed, const 
     if (t == 0) ws.ttot[blockIdx.x] = rowbase;
 }
 
-// R: one chunk per workgroup (resolve_chunk)
+// R, two passes (no workgroup waits for another: two processes' decodes may share a GPU):
+// the per-chunk resolve up to the kept ranks (resolve_chunk<kSplit>), then the records
+// (write_runs) once every chunk's kept count is in ws.cres
 constexpr int kToffLds = 1024;
 __global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int64_t C,
                                                     IslWs ws, IslOut o) {
     __shared__ ResolveLds L;
-    __shared__ Cnt5 s_to[kToffLds];
-    resolve_chunk<false, kToffLds>(packed, C, ws, o, blockIdx.x, L, s_to);
+    resolve_chunk<false, kToffLds, true>(packed, C, ws, o, blockIdx.x, L, nullptr);
+}
+__global__ __launch_bounds__(kIT) void k_isl_write(const uint32_t* packed, int64_t C, IslWs ws,
+                                                  IslOut o) {
+    __shared__ long long s_part[kIT / 64];
+    write_runs(packed, C, ws, o, blockIdx.x, s_part);
 }
 
 }  // namespace
@@ -210,18 +222,18 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
                           cpg_island* out, int64_t cap, int64_t* count, uint32_t* status,
                           hipStream_t s, unsigned long long* flags, const int64_t* base_in) {
     IslWs ws = carve_isl(wsp, nchunks, chunk_len, kTW);
-    if (ws.bytes > ws_bytes || !flags) return hipErrorInvalidValue;
-    ws.flags = flags;
+    if (ws.bytes > ws_bytes) return hipErrorInvalidValue;
+    (void)flags;   // the separate kernels need no look-back flags
     if (nchunks == 0)
         return base_in ? hipMemcpyAsync(count, base_in, sizeof(int64_t), hipMemcpyDeviceToDevice, s)
                        : hipMemsetAsync(count, 0, sizeof(int64_t), s);
     hipLaunchKernelGGL(k_isl_tile, dim3((unsigned)(nchunks * ws.ntile)), dim3(kTT), 0, s, packed,
                        sign, chunk_len, ws);
-    // a fresh tag per call for the look-back flags (their own workspace slot: stale words are
-    // earlier calls' flags, whose tags never match)
-    const IslOut o{out, cap, count, base_in, first_chunk, lookback_epoch(), status, nchunks};
+    const IslOut o{out, cap, count, base_in, first_chunk, 0u, status, nchunks};
     hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed,
                        chunk_len, ws, o);
+    hipLaunchKernelGGL(k_isl_write, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, chunk_len,
+                       ws, o);
     return hipGetLastError();
 }
 

@@ -42,6 +42,10 @@ def lib():
         L.orc_ingest_train.restype = _I64
         L.orc_ingest_decode.argtypes = [_P, _I64, _P, _I64, _P]
         L.orc_ingest_decode.restype = _I64
+        L.orc_ingest_train_at.argtypes = [_P, _I64, _P, _I64, C.c_uint32, _P]
+        L.orc_ingest_train_at.restype = _I64
+        L.orc_ingest_decode_at.argtypes = [_P, _I64, _P, _I64, C.c_uint32, _P, _P]
+        L.orc_ingest_decode_at.restype = _I64
         L.orc_viterbi8.argtypes = [_P, _P, _I64, _P]
         L.orc_viterbi8.restype = C.c_double
         L.orc_viterbi2.argtypes = [_P, _P, _I64, _P]
@@ -97,6 +101,25 @@ def ingest_decode(txt: bytes):
     n = lib().orc_ingest_decode(_ptr(buf), len(buf), _ptr(out), cap, C.byref(crash))
     assert n >= 0
     return out[:n], bool(crash.value)
+
+
+def ingest_at(txt: bytes, mode: int, count0: int):
+    """The reader of `mode` (0 training, 1 decode) starting from Java count = count0 with an
+    empty list (the 2^32-wrap test hook).  Returns (symbols, crash_byte or -1)."""
+    buf = np.frombuffer(txt, np.uint8).copy()
+    chunk = 0x10000 if mode == 0 else 0x100000
+    extra = 0 if mode else int(np.count_nonzero(~np.isin(buf, np.frombuffer(b"ACGTacgt", np.uint8))))
+    cap = (len(buf) // chunk + 2 + extra) * chunk
+    out = np.zeros(cap, np.uint8)
+    cb = C.c_int64(-1)
+    if mode == 0:
+        n = lib().orc_ingest_train_at(_ptr(buf), len(buf), _ptr(out), cap, count0, C.byref(cb))
+    else:
+        crash = C.c_int(0)
+        n = lib().orc_ingest_decode_at(_ptr(buf), len(buf), _ptr(out), cap, count0,
+                                       C.byref(crash), C.byref(cb))
+    assert n >= 0
+    return out[:n], int(cb.value)
 
 
 def viterbi8(model: np.ndarray, obs: np.ndarray):

@@ -49,19 +49,27 @@ static inline int sym_of(uint8_t ch) {
 
 /* :112-145.  `count` is a Java int: the chunk test (count != 0 && count % 0x10000 == 0)
  * is evaluated after EVERY character, so a non-ACGT character read while count sits on a
- * multiple emits another chunk from the (empty) list: DenseVector(0x10000) all 0.0 = 'A'. */
-int64_t orc_ingest_train(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap) {
-    uint32_t count = 0;              /* Java int, wraps */
+ * multiple emits another chunk from the (empty) list: DenseVector(0x10000) all 0.0 = 'A'.
+ * At 2^32 bases `count` wraps to 0 and the test is skipped: the list keeps its 65,536
+ * bases, grows to 131,072 by the next multiple, and there `inputVector.set(65536, …)`
+ * (:133-134) throws — the training run dies at the valid byte that brings count to
+ * 2^32 + 65,536 (*crash_byte; returns the symbols of the chunks written before it).
+ * count0: the Java `count` before the first byte (test hook: a stream that has already
+ * read and committed count0 bases; a multiple of 65,536 below 2^32). */
+int64_t orc_ingest_train_at(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap,
+                            uint32_t count0, int64_t* crash_byte) {
+    uint32_t count = count0;         /* Java int, wraps */
     int64_t listlen = 0, out = 0;
-    uint8_t* list = (uint8_t*)malloc(CPG_TRAIN_CHUNK);
+    *crash_byte = -1;
+    uint8_t* list = (uint8_t*)malloc(2 * CPG_TRAIN_CHUNK);   /* one skipped test at most */
     for (int64_t k = 0; k < n; ++k) {
         int v = sym_of(txt[k]);
         if (v != -1) {
-            if (listlen >= CPG_TRAIN_CHUNK) { free(list); return -2; } /* set() out of range */
             list[listlen++] = (uint8_t)v;
             count++;
         }
         if (count != 0 && (count & 0xFFFFu) == 0) {
+            if (listlen > CPG_TRAIN_CHUNK) { *crash_byte = k; break; }   /* set(65536) */
             if (out + CPG_TRAIN_CHUNK > cap) { free(list); return -1; }
             memset(syms + out, 0, CPG_TRAIN_CHUNK);          /* new DenseVector: zeros */
             memcpy(syms + out, list, (size_t)listlen);        /* :133-135 */
@@ -73,30 +81,51 @@ int64_t orc_ingest_train(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t c
     return out;                       /* tail (count % 65536 bases) never written */
 }
 
-/* :238-259 */
-int64_t orc_ingest_decode(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap,
-                          int* crash) {
-    uint32_t count = 0;
+int64_t orc_ingest_train(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap) {
+    int64_t cb;
+    const int64_t r = orc_ingest_train_at(txt, n, syms, cap, 0u, &cb);
+    return cb >= 0 ? -2 : r;
+}
+
+/* :238-259.  At 2^32 bases `count` wraps to 0 and the test is skipped: the list keeps its
+ * 2^20 bases and keeps growing; at the next multiple the loop copies get(0..2^20-1) — the
+ * held chunk — and clear() drops the 2^20 bases read after the wrap.  No exception; the
+ * chunks after it are shifted (their `chunk` index counts decoded chunks, :287).  A
+ * non-ACGT byte read while count == 0 fires nothing.  count0 as for the training reader
+ * (a multiple of 2^20 below 2^32). */
+int64_t orc_ingest_decode_at(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap,
+                             uint32_t count0, int* crash, int64_t* crash_byte) {
+    uint32_t count = count0;
     int64_t listlen = 0, out = 0;
     *crash = 0;
-    uint8_t* list = (uint8_t*)malloc(CPG_DECODE_CHUNK + 1);
+    *crash_byte = -1;
+    uint8_t* list = (uint8_t*)malloc(2 * CPG_DECODE_CHUNK);  /* one skipped test at most */
     for (int64_t k = 0; k < n; ++k) {
         int v = sym_of(txt[k]);
         if (v != -1) {
-            if (listlen > CPG_DECODE_CHUNK) { *crash = 1; break; }
             list[listlen++] = (uint8_t)v;
             count++;
         }
         if (count != 0 && (count & 0xFFFFFu) == 0) {
-            if (listlen < CPG_DECODE_CHUNK) { *crash = 1; break; }  /* get(i) on short list */
+            if (listlen < CPG_DECODE_CHUNK) {              /* get(i) on a short list */
+                *crash = 1;
+                *crash_byte = k;
+                break;
+            }
             if (out + CPG_DECODE_CHUNK > cap) { free(list); return -1; }
-            memcpy(syms + out, list, CPG_DECODE_CHUNK);
+            memcpy(syms + out, list, CPG_DECODE_CHUNK);     /* get(0 .. 2^20-1) */
             out += CPG_DECODE_CHUNK;
-            listlen = 0;
+            listlen = 0;                                     /* clear(): drops the rest */
         }
     }
     free(list);
     return out;
+}
+
+int64_t orc_ingest_decode(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap,
+                          int* crash) {
+    int64_t cb;
+    return orc_ingest_decode_at(txt, n, syms, cap, 0u, crash, &cb);
 }
 
 /* Mahout HmmAlgorithms.viterbiAlgorithm(sequence, delta, phi, model, obs, scaled=true),

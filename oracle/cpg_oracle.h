@@ -35,6 +35,14 @@ int64_t orc_ingest_train(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t c
  * of the chunks decoded before it. */
 int64_t orc_ingest_decode(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap,
                           int* crash);
+/* The same readers starting from Java `count` = count0 with an empty list (a test hook for
+ * the 2^32 wrap of the int counter: count0 a multiple of the chunk below 2^32).  The
+ * training reader's crash at the wrap (DenseVector.set(65536), :133-134) and the decode
+ * reader's (get(i) on an empty list) report the input byte in *crash_byte (-1: none). */
+int64_t orc_ingest_train_at(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap,
+                            uint32_t count0, int64_t* crash_byte);
+int64_t orc_ingest_decode_at(const uint8_t* txt, int64_t n, uint8_t* syms, int64_t cap,
+                             uint32_t count0, int* crash, int64_t* crash_byte);
 
 /* Mahout HmmAlgorithms.viterbiAlgorithm(model, obs, scaled=true), 8 states, Math.log in
  * the inner loop exactly as Mahout does.  states_out[T]; returns max final delta. */

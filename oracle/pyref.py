@@ -38,13 +38,17 @@ def _log(x: float) -> float:
     return math.log(x) if x > 0 else (-math.inf if x == 0 else math.nan)
 
 
-def ingest(txt: bytes, chunk: int):
+def ingest(txt: bytes, chunk: int, count0: int = 0):
     """:112-145 (chunk=0x10000) / :238-259 (chunk=0x100000), quirk-faithful.
 
     Returns (list of chunks as lists of symbols, crash_flag).  For the training chunk
     size an empty list at a chunk multiple yields an all-zero chunk (new DenseVector);
-    for the decode size it is the reference's crash (get(i) on an empty list)."""
-    count = 0
+    for the decode size it is the reference's crash (get(i) on an empty list).
+    `count` is a Java int: at 2^32 it wraps to 0 and the test is skipped, so the list keeps
+    its chunk and grows; at the next multiple the training reader's DenseVector.set(65536)
+    throws (crash), the decode reader copies get(0 .. 2^20-1) and clear() drops the rest.
+    count0 = the Java count before the first byte (test hook; a multiple of `chunk`)."""
+    count = count0 & 0xFFFFFFFF
     lst: list[int] = []
     chunks = []
     for ch in txt:
@@ -54,9 +58,11 @@ def ingest(txt: bytes, chunk: int):
             count = (count + 1) & 0xFFFFFFFF
         if count != 0 and count % chunk == 0:
             if chunk == 0x100000 and len(lst) < chunk:
-                return chunks, True
+                return chunks, True                 # get(i) on an empty list
+            if chunk == 0x10000 and len(lst) > chunk:
+                return chunks, True                 # DenseVector(0x10000).set(0x10000, ...)
             c = [0] * chunk
-            c[: len(lst)] = lst
+            c[: min(len(lst), chunk)] = lst[:chunk]
             chunks.append(c)
             lst = []
     return chunks, False

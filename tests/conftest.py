@@ -7,6 +7,10 @@ import pytest
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
+# development only: run the suite against a variant build's package tree
+# (tools/build_variant.sh makes build/abl/pkg_<name>/cpgisland_amd with that libcpg.so)
+if os.environ.get("CPG_DEV_PKG"):
+    sys.path.insert(0, os.environ["CPG_DEV_PKG"])
 
 
 def pytest_configure(config):

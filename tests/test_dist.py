@@ -7,6 +7,7 @@ code that runs unchanged over RCCL on the GPU box — are checked against the un
 """
 import os
 import socket
+import sys
 
 import numpy as np
 import pytest
@@ -282,3 +283,46 @@ def test_bench_c3_halo_p2p_and_island_gather(world):
     res = sorted([q.get() for _ in range(world)])
     assert any(r[1] > 0 for r in res)             # some rank's last chunk needed the halo
     assert all(r[2] for r in res) and all(r[3] for r in res)
+
+
+_RANK_WORKER = r'''
+import os, sys, torch, torch.distributed as dist
+dist.init_process_group("gloo")
+r, w = dist.get_rank(), dist.get_world_size()
+assert int(os.environ["LOCAL_RANK"]) == r and os.environ["MASTER_ADDR"] == "127.0.0.1"
+t = torch.tensor([r + 1], dtype=torch.int64)
+dist.all_reduce(t)
+if r == 0:
+    print("SUM", int(t.item()), w, flush=True)
+dist.destroy_process_group()
+sys.exit(int(os.environ.get("FAIL_RANK", "-1")) == r)
+'''
+
+
+def test_bench_launcher_starts_n_ranks(tmp_path, capfd):
+    """bench.py --gpus N without WORLD_SIZE starts N rank processes itself (the launcher the
+    driver's `python bench.py --gpus N` relies on): RANK / LOCAL_RANK / WORLD_SIZE / MASTER_*
+    set, one collective over gloo, rank 0's line on stdout; a failing rank fails the launch."""
+    import bench
+    w = tmp_path / "worker.py"
+    w.write_text(_RANK_WORKER)
+    env_keep = {k: os.environ.pop(k) for k in ("RANK", "WORLD_SIZE", "FAIL_RANK") if k in os.environ}
+    try:
+        assert bench.launch_ranks(3, [sys.executable, str(w)]) == 0
+        out = capfd.readouterr().out.splitlines()    # (gloo itself prints connection lines)
+        assert [x for x in out if x.startswith("SUM")] == ["SUM 6 3"]
+        os.environ["FAIL_RANK"] = "1"
+        assert bench.launch_ranks(2, [sys.executable, str(w)]) != 0
+    finally:
+        os.environ.pop("FAIL_RANK", None)
+        os.environ.update(env_keep)
+
+
+def test_bench_rejects_world_size_mismatch():
+    """Launched with WORLD_SIZE != --gpus, bench.py exits non-zero before touching a GPU."""
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, WORLD_SIZE="2", RANK="0", LOCAL_RANK="0")
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "4"],
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert p.returncode != 0 and "WORLD_SIZE=2 but --gpus 4" in p.stderr

@@ -175,3 +175,54 @@ def test_large_synthetic_text_roundtrip(gpu_ctx, torch_dev):
         assert nb == (n + 1) // chunk * chunk + int(r[4]) * chunk
         if r[4] == 0:
             assert np.array_equal(got, ref)
+
+
+def _gpu_at(ctx, txt, mode, count0, cap):
+    from cpgisland_amd import _lib
+    gp = np.zeros(cap // 16 + 8, np.uint32)
+    nb = C.c_int64()
+    rc = _lib.lib.cpgx_ingest_gpu_at(ctx.handle, txt, len(txt), mode, 1, _lib.ptr(gp), cap,
+                                     C.byref(nb), C.c_uint32(count0))
+    msg = _lib.lib.cpg_last_error().decode() if rc else ""
+    return rc, nb.value, pr.unpack(gp, nb.value), msg
+
+
+def _crash_byte(msg):
+    import re
+    m = re.search(r"byte (\d+) ", msg)
+    return int(m.group(1)) if m else -1
+
+
+WRAP_CASES = [   # (mode, count0, bases, FASTA width): the Java int count wraps inside the text
+    (1, (1 << 32) - 2 * DECODE, 6 * DECODE + 77, 60),    # held chunk decoded, next dropped
+    (1, (1 << 32) - 3 * DECODE, 7 * DECODE + 5, 61),
+    (1, (1 << 32) - 2 * DECODE, 2 * DECODE + 5000, 60),  # ends inside the dropped window
+    (0, (1 << 32) - 2 * TRAIN, 4 * TRAIN + 9, 64),       # all-A chunk, then the crash
+    (0, (1 << 32) - 2 * TRAIN, 3 * TRAIN - 1, 60),       # ends before the crash
+    (0, (1 << 32) - 5 * TRAIN, 9 * TRAIN, 70),
+]
+
+
+@pytest.mark.parametrize("case", WRAP_CASES, ids=[f"wrap{i}" for i in range(len(WRAP_CASES))])
+def test_count_wrap_device_matches_host_and_oracle(gpu_ctx, case):
+    """The device reader at the Java int count's 2^32 wrap (test hook cpgx_ingest_gpu_at:
+    count starts at count0) against the host reader, the C oracle and the pure-Python one:
+    committed bases, status, crash byte (tests/test_ingest_wrap.py derives the rules)."""
+    from cpgisland_amd import _lib
+    mode, c0, nbases, width = case
+    rng = np.random.default_rng(nbases)
+    txt = fasta(rng, nbases, width, header=b"")   # count0 sits on a multiple
+    chunk = TRAIN if mode == 0 else DECODE
+    cap = (nbases // chunk + 8) * chunk + len(txt) // width * chunk * (mode == 0)
+    rc, nb, gp, msg = _gpu_at(gpu_ctx, txt, mode, c0, cap)
+    hp_packed = np.zeros(cap // 16 + 8, np.uint32)
+    hnb = C.c_int64()
+    hrc = _lib.lib.cpgx_ingest_at(txt, len(txt), mode, 1, _lib.ptr(hp_packed), cap,
+                                  C.byref(hnb), C.c_uint32(c0))
+    hmsg = _lib.lib.cpg_last_error().decode() if hrc else ""
+    assert (rc, nb) == (hrc, hnb.value)
+    assert np.array_equal(gp, pr.unpack(hp_packed, nb))
+    ref, cb = co.ingest_at(txt, mode, c0)
+    assert np.array_equal(gp, ref)
+    assert _crash_byte(msg) == _crash_byte(hmsg) == cb
+    assert (rc == _lib.CPG_E_REF_CRASH) == (cb >= 0)

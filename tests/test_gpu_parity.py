@@ -267,7 +267,7 @@ def _labelled(kind, N, seed):
     return obs, sg.astype(np.uint8)
 
 
-@pytest.mark.parametrize("C", [256, 4096, 65536])
+@pytest.mark.parametrize("C", [256, 768, 4096, 12288, 65536])   # 768 / 12288: k_count_main<false>
 @pytest.mark.parametrize("kind", ["random", "synth", "plus", "minus", "alternating", "runs"])
 def test_counts_bit_exact(gpu_ctx, torch_dev, C, kind):
     from cpgisland_amd import device as D
@@ -280,9 +280,9 @@ def test_counts_bit_exact(gpu_ctx, torch_dev, C, kind):
 
 @pytest.mark.parametrize("kind", ["synth", "plus"])
 def test_counts_many_batches_vs_oracle(gpu_ctx, torch_dev, kind):
-    """160 Mbp: ~19 blocks per lane of the count grid, several batches and flushes per lane;
-    all-A / all-'+' puts 63 transitions of one class in every block (the 16-bit fields of a
-    wave sum would overflow without the per-batch flush)."""
+    """160 Mbp: ~19 blocks per lane of the count grid, several batches per lane; all-A /
+    all-'+' puts 63 transitions of one class in every block, so every lane's 32-bit moment
+    registers and the island moments' LDS replicas take their largest per-block increments."""
     from cpgisland_amd import device as D
     N = 160_000_000 + 4321
     if kind == "synth":
@@ -441,21 +441,31 @@ def test_islands_long_overflow_island(gpu_ctx, torch_dev):
 
 
 def test_islands_lookback_timeout_is_an_error(gpu_ctx):
-    """The island kernel's look-back over earlier chunks' kept counts is a bounded spin.
-    libcpg_isl_timeout.so is built with that bound forced to 0 (CPG_ISL_SPIN_LIMIT=0), so
-    every chunk after the first gives up: the call must fail with CPG_E_DEVICE (status bit
-    ST_LOOKBACK_TIMEOUT via cpg_sync) instead of returning records at wrong offsets."""
+    """Only the fused decode's island resolve (cpg_decode_d, <= 256 chunks of a 64 Ki
+    multiple: the chunk's last traceback workgroup) finds its first record by a look-back over
+    earlier chunks' kept counts, a bounded spin.  libcpg_isl_timeout.so is built with that
+    bound forced to 0 (CPG_ISL_SPIN_LIMIT=0), so every chunk after the first gives up: the
+    call must fail with CPG_E_DEVICE (status bit ST_LOOKBACK_TIMEOUT via cpg_sync) instead of
+    returning records at wrong offsets.  The separate island kernels (cpg_islands*, and the
+    decode past 256 chunks) place records by a second kernel over the per-chunk counts: no
+    workgroup waits for another, so the same library returns the oracle's records there."""
     import ctypes as C
     import os
-    from cpgisland_amd import _lib
+    import torch
+    from cpgisland_amd import HmmModel, _lib
+    from cpgisland_amd import device as D
     path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libcpg_isl_timeout.so")
     assert os.path.exists(path), "build it: make -C cpgisland_amd/csrc"
     lib = C.CDLL(path)
     lib.cpg_open.argtypes = [C.c_int, C.c_void_p]
     lib.cpg_close.argtypes = [C.c_void_p]
     lib.cpg_last_error.restype = C.c_char_p
+    lib.cpg_sync.argtypes = [C.c_void_p, C.c_void_p]
     lib.cpg_islands.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
                                 C.c_void_p, C.c_int64, C.c_void_p]
+    lib.cpg_decode_d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
+                                 C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
+                                 C.c_void_p, C.c_void_p]
     rng = np.random.default_rng(7)
     CL, nch = 4096, 8
     states = np.concatenate([np.resize(_rand_states(rng), CL) for _ in range(nch)])
@@ -463,29 +473,44 @@ def test_islands_lookback_timeout_is_an_error(gpu_ctx):
     sign = np.ascontiguousarray(pr.pack_bits((states < 4).astype(np.uint8)).astype(np.uint32))
     out = np.zeros(4096, co.ISLAND_DTYPE)
     cnt = C.c_int64(0)
+    exp = np.concatenate([co.islands(states[c * CL:(c + 1) * CL], c) for c in range(nch)])
+    dev = torch.device("cuda:0")
+    n2, c2l = 8 * 65536, 65536
+    p2, _ = D.synth_host(11, 0, n2)
+    m = np.ascontiguousarray(co.initial_model())
+    dp2 = D.to_device(np.concatenate([p2, np.zeros(8, np.uint32)]), dev)
+    so = torch.zeros(D.words32(n2) + 4, dtype=torch.int32, device=dev)
+    sc = torch.zeros(8, dtype=torch.float64, device=dev)
+    io = torch.zeros((4096, 32), dtype=torch.uint8, device=dev)
+    ic = torch.zeros(1, dtype=torch.int64, device=dev)
     ctx = C.c_void_p()
     assert lib.cpg_open(0, C.byref(ctx)) == 0
     try:
         rc = lib.cpg_islands(ctx, packed.ctypes.data, sign.ctypes.data, nch * CL, CL,
                              out.ctypes.data, len(out), C.byref(cnt))
+        assert rc == 0, lib.cpg_last_error()
+        assert np.array_equal(out[:cnt.value], exp)
+        torch.cuda.synchronize()
+        rc = lib.cpg_decode_d(ctx, m.ctypes.data, dp2.data_ptr(), n2, c2l, 0, so.data_ptr(),
+                              sc.data_ptr(), io.data_ptr(), 4096, ic.data_ptr(), None)
+        assert rc == 0
+        rc = lib.cpg_sync(ctx, None)
         assert rc == _lib.CPG_E_DEVICE, rc
         assert b"look-back" in lib.cpg_last_error()
-        # the status word was consumed: the same context works again for one chunk
+        # the status word was consumed: the same context works again
         rc1 = lib.cpg_islands(ctx, packed.ctypes.data, sign.ctypes.data, CL, CL,
                               out.ctypes.data, len(out), C.byref(cnt))
         assert rc1 == 0
-        exp = co.islands(states[:CL], 0)
-        assert np.array_equal(out[:cnt.value], exp)
+        assert np.array_equal(out[:cnt.value], co.islands(states[:CL], 0))
     finally:
         lib.cpg_close(ctx)
-    # the product library on the same input: no timeout, oracle records
-    from cpgisland_amd import device as D
-    import torch
-    dev = torch.device("cuda:0")
-    dp, ds = _dev_genome(packed, sign, dev)
-    o2, c2 = D.islands(gpu_ctx, dp, ds, nch * CL, CL)
-    exp = np.concatenate([co.islands(states[c * CL:(c + 1) * CL], c) for c in range(nch)])
-    assert np.array_equal(D.islands_to_numpy(o2, c2), exp)
+    # the product library: the fused decode's records equal the separate calls' (no timeout)
+    so2, sc2, io2, ic2 = D.decode(gpu_ctx, HmmModel.initial(), dp2, n2, c2l)
+    so3, _ = D.viterbi(gpu_ctx, HmmModel.initial(), dp2, n2, c2l)
+    o3, c3 = D.islands(gpu_ctx, dp2, so3, n2, c2l)
+    torch.cuda.synchronize()
+    gpu_ctx.sync()
+    assert np.array_equal(D.islands_to_numpy(io2, ic2), D.islands_to_numpy(o3, c3))
 
 
 def test_islands_capacity(gpu_ctx, torch_dev, golden):

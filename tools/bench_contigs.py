@@ -15,6 +15,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("CPG_DEV_PKG"):   # a variant tree from tools/build_variant.sh
+    sys.path.insert(0, os.environ["CPG_DEV_PKG"])
 from cpgisland_amd import Context, HmmModel  # noqa: E402
 from cpgisland_amd import device as D  # noqa: E402
 

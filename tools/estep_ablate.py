@@ -1,6 +1,8 @@
-"""Time the E-step kernel of one libcpg build (CPG_LIB_OVERRIDE) on 46 Mbp (dev tool)."""
+"""Time the E-step kernel of one libcpg build (CPG_DEV_PKG: a tree made by tools/build_variant.sh) on 46 Mbp (dev tool)."""
 import os, sys, time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("CPG_DEV_PKG"):   # a variant tree from tools/build_variant.sh
+    sys.path.insert(0, os.environ["CPG_DEV_PKG"])
 import torch
 from cpgisland_amd import Context, HmmModel
 from cpgisland_amd import device as D
@@ -18,7 +20,7 @@ ts = []
 for _ in range(10):
     a.record(); D.bw_estep(ctx, m, dp, N, 65536, out=out); b.record(); torch.cuda.synchronize()
     ts.append(a.elapsed_time(b))
-print(os.environ.get("CPG_LIB_OVERRIDE", "default"), "estep ms median %.4f min %.4f" % (sorted(ts)[5], min(ts)))
+print(os.environ.get("CPG_DEV_PKG", "default"), "estep ms median %.4f min %.4f" % (sorted(ts)[5], min(ts)))
 # accuracy of this build on 32 chunks vs the oracle (max relative error over non-zero counts)
 import numpy as np
 from oracle import coracle as co, pyref as pr

@@ -6,6 +6,8 @@ Warmed up for ~40 ms first (the clock ramp, profiles/r03_v1/startup_probe.txt)."
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("CPG_DEV_PKG"):   # a variant tree from tools/build_variant.sh
+    sys.path.insert(0, os.environ["CPG_DEV_PKG"])
 import torch  # noqa: E402
 from cpgisland_amd import Context, HmmModel  # noqa: E402
 from cpgisland_amd import device as D  # noqa: E402

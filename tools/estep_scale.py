@@ -2,6 +2,8 @@
 the grid's round quantisation on 256 CUs."""
 import os, sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("CPG_DEV_PKG"):   # a variant tree from tools/build_variant.sh
+    sys.path.insert(0, os.environ["CPG_DEV_PKG"])
 import torch
 from cpgisland_amd import Context, HmmModel
 from cpgisland_amd import device as D
@@ -22,4 +24,4 @@ for k in [int(x) for x in os.environ.get("CHUNKS", "64 128 256 384 512 640 702 7
         a.record(); D.bw_estep(ctx, m, dp, N, 65536, out=out); b.record(); torch.cuda.synchronize()
         ts.append(a.elapsed_time(b))
     t = sorted(ts)[3]
-    print(f"{os.path.basename(os.environ.get('CPG_LIB_OVERRIDE', 'default'))} chunks {k:5d} ms {t:.4f} per-chunk-us {t*1e3/k:.3f}", flush=True)
+    print(f"{os.path.basename(os.environ.get('CPG_DEV_PKG', 'default'))} chunks {k:5d} ms {t:.4f} per-chunk-us {t*1e3/k:.3f}", flush=True)

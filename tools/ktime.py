@@ -1,8 +1,10 @@
 """Median time (HIP events) of one hot-path phase on 46 Mbp for the libcpg build named by
-CPG_LIB_OVERRIDE (dev tool).  PHASE = estep | counts | train | viterbi | islands."""
+CPG_DEV_PKG (dev tool).  PHASE = estep | counts | train | viterbi | islands."""
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("CPG_DEV_PKG"):   # a variant tree from tools/build_variant.sh
+    sys.path.insert(0, os.environ["CPG_DEV_PKG"])
 import torch  # noqa: E402
 from cpgisland_amd import Context, HmmModel  # noqa: E402
 from cpgisland_amd import device as D  # noqa: E402
@@ -24,7 +26,7 @@ ph = {"estep": lambda: D.bw_estep(ctx, m, dp, N, 65536, out=ec),
       "train": lambda: D.train_pass(ctx, m, dp, ds, N, 65536, estep_out=ec, counts_out=lc),
       "viterbi": lambda: D.viterbi(ctx, m, dp, N, 1 << 20, sign_out=so),
       "islands": lambda: D.islands(ctx, dp, so, N, 1 << 20, cap=1 << 20, out=iout, count=icnt)}
-name = os.path.basename(os.environ.get("CPG_LIB_OVERRIDE", "") or "default")
+name = os.path.basename(os.environ.get("CPG_DEV_PKG", "") or "default")
 for phase in os.environ.get("PHASES", "counts").split():
     f = ph[phase]
     for _ in range(3):

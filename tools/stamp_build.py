@@ -1,7 +1,7 @@
 """Dev tool: build/abl/libcpg_stamp.so — the library with per-phase wall-clock stamps
 (s_memrealtime, 100 MHz) in the fused training pass, inserted into a COPY of the sources at
 anchor lines (the product sources carry no instrumentation).  Read them with
-tools/stamp_estep.py (CPG_LIB_OVERRIDE=build/abl/libcpg_stamp.so)."""
+tools/stamp_estep.py (CPG_DEV_PKG=build/abl/pkg_stamp)."""
 import os
 import shutil
 import subprocess

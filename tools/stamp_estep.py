@@ -1,9 +1,11 @@
 """Per-phase wall-clock stamps (s_memrealtime, 100 MHz) of the fused training pass's
-workgroups, from an ABL_STAMP build (dev tool: CPG_LIB_OVERRIDE=build/abl/libcpg_stamp.so)."""
+workgroups, from an ABL_STAMP build (dev tool: CPG_DEV_PKG=build/abl/pkg_stamp)."""
 import ctypes
 import os
 import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+if os.environ.get("CPG_DEV_PKG"):   # a variant tree from tools/build_variant.sh
+    sys.path.insert(0, os.environ["CPG_DEV_PKG"])
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 from cpgisland_amd import Context, HmmModel  # noqa: E402
