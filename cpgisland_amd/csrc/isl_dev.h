@@ -495,7 +495,7 @@ __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C,
     const int t = threadIdx.x, nl = blockDim.x;
     const int64_t maxr = C / 2 + 1;
     const uint32_t* pk = packed + c * (C / 16);
-    const bool in_lds = !kSplit && ws.ntile <= kToff;   // kSplit: write_runs reads ws.toff
+    const bool in_lds = ws.ntile <= kToff;
     Cnt5 carry{0, 0, 0, 0, 0};
     for (int64_t b = 0, it = 0; b < ws.ntile; b += nl, ++it) {
         const int64_t i = b + t;
@@ -506,7 +506,8 @@ __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C,
         if (i < ws.ntile) {
             const Cnt5 oo = cadd(e, carry);
             if (in_lds) s_to[i] = oo;
-            else ws.toff[c * ws.ntile + i] = oo;
+            // (kSplit: write_runs, the next kernel, reads the offsets from ws.toff)
+            if (!in_lds || kSplit) ws.toff[c * ws.ntile + i] = oo;
         }
         carry = cadd(carry, tot);
     }

@@ -182,7 +182,8 @@ constexpr int kToffLds = 1024;
 __global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int64_t C,
                                                     IslWs ws, IslOut o) {
     __shared__ ResolveLds L;
-    resolve_chunk<false, kToffLds, true>(packed, C, ws, o, blockIdx.x, L, nullptr);
+    __shared__ Cnt5 s_to[kToffLds];
+    resolve_chunk<false, kToffLds, true>(packed, C, ws, o, blockIdx.x, L, s_to);
 }
 __global__ __launch_bounds__(kIT) void k_isl_write(const uint32_t* packed, int64_t C, IslWs ws,
                                                   IslOut o) {
