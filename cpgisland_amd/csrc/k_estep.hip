@@ -285,6 +285,19 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 // tools/ab_libs.sh; a few spills, none of them in the main loop's steady state).  At 4 per
 // SIMD (122 VGPRs, no spills) the kernel alone is as fast; 6 per SIMD spills 38.
 constexpr int kWavesPerEU = 5;
+// kRep (147.5 KB of LDS: one workgroup per CU, nothing co-resides): 4 waves per SIMD, so the
+// whole 128-VGPR share of a wave is this kernel's
+#ifndef CPG_EST_WPE_REP
+#define CPG_EST_WPE_REP 4
+#endif
+constexpr int kWavesPerEURep = CPG_EST_WPE_REP;
+// table rows issued this many two-position blocks ahead of their use (forward / backward)
+#ifndef CPG_EST_FPD_REP
+#define CPG_EST_FPD_REP 1
+#endif
+#ifndef CPG_EST_PFD_REP
+#define CPG_EST_PFD_REP 1
+#endif
 // kCnt: the fused training pass — each lane also counts its 64 bases' labelled transitions
 // (count_dev.h; sign = the label bits), added into the count accumulators cacc, and the last
 // workgroup finalizes both (cout: cpg_counts_i64).  Needs >= 256 lanes (chunks >= 16 Ki).
@@ -293,12 +306,13 @@ constexpr int kWavesPerEU = 5;
 // (40 KB more LDS: 147.5 KB per workgroup); otherwise forward rows from the shared LDS rows
 // (bank conflicts) and backward rows from L1.  See launch_estep for when.
 template <bool kCnt, bool kRep>
-__global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(kWavesPerEU)))
-void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
-                   unsigned long long* __restrict__ acc, const double2* __restrict__ gtab,
-                   unsigned int* done, double* __restrict__ out,
-                   const uint32_t* __restrict__ sign, unsigned long long* __restrict__ cacc,
-                   int64_t* __restrict__ cout) {
+__device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32_t* __restrict__ packed,
+                                            int64_t C, unsigned long long* __restrict__ acc,
+                                            const double2* __restrict__ gtab, unsigned int* done,
+                                            double* __restrict__ out,
+                                            const uint32_t* __restrict__ sign,
+                                            unsigned long long* __restrict__ cacc,
+                                            int64_t* __restrict__ cout) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves
@@ -579,7 +593,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         // the rows are issued kFPD steps ahead (the scheduling barrier keeps them there: the
         // compiler had waited for each step's reads right before using them, one LDS round
         // trip on every step of the chain)
-        constexpr int kFPD = 1;   // (2: one spill at 96 VGPRs and no faster, measured)
+        constexpr int kFPD = kRep ? CPG_EST_FPD_REP : 1;   // (2: one spill at 96 VGPRs and no faster)
         double2 fa[kFPD + 1], fb[kFPD + 1];
 #pragma unroll
         for (int j = 0; j < kFPD; ++j) {
@@ -608,7 +622,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
             yP *= r;
             yM *= r;
         }
-        constexpr int kPFD = 1;   // backward rows loaded this many blocks ahead
+        constexpr int kPFD = kRep ? CPG_EST_PFD_REP : 1;   // backward rows this many blocks ahead
         double2 qa[kPFD + 1], qb[kPFD + 1];
 #pragma unroll
         for (int j = 0; j < kPFD; ++j) {
@@ -687,6 +701,26 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
         if (kCnt) cnt::fin_store(cacc, craw, cout, te, nl);
         reset_done(done);
     }
+}
+
+template <bool kCnt>
+__global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(kWavesPerEU)))
+void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
+                   unsigned long long* __restrict__ acc, const double2* __restrict__ gtab,
+                   unsigned int* done, double* __restrict__ out,
+                   const uint32_t* __restrict__ sign, unsigned long long* __restrict__ cacc,
+                   int64_t* __restrict__ cout) {
+    estep_chunk<kCnt, false>(model, packed, C, acc, gtab, done, out, sign, cacc, cout);
+}
+// the long launches' form (kRep): lane-private row copies, the registers of 4 waves per SIMD
+template <bool kCnt>
+__global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(kWavesPerEURep)))
+void k_estep_chunk_rep(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
+                       unsigned long long* __restrict__ acc, const double2* __restrict__ gtab,
+                       unsigned int* done, double* __restrict__ out,
+                       const uint32_t* __restrict__ sign, unsigned long long* __restrict__ cacc,
+                       int64_t* __restrict__ cout) {
+    estep_chunk<kCnt, true>(model, packed, C, acc, gtab, done, out, sign, cacc, cout);
 }
 
 
@@ -817,11 +851,11 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
         unsigned int* done =
             parts == PART_ALL ? reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep) : nullptr;
         if (nchunks >= kEstRepMinChunks)
-            hipLaunchKernelGGL((k_estep_chunk<false, true>), dim3((unsigned)nchunks), dim3(lanes),
+            hipLaunchKernelGGL((k_estep_chunk_rep<false>), dim3((unsigned)nchunks), dim3(lanes),
                                estep_lds(lanes, true), s, model, packed, C, acc, gtab, done, out,
                                nullptr, nullptr, nullptr);
         else
-            hipLaunchKernelGGL((k_estep_chunk<false, false>), dim3((unsigned)nchunks), dim3(lanes),
+            hipLaunchKernelGGL((k_estep_chunk<false>), dim3((unsigned)nchunks), dim3(lanes),
                                estep_lds(lanes, false), s, model, packed, C, acc, gtab, done, out,
                                nullptr, nullptr, nullptr);
         if (done) return hipGetLastError();
@@ -845,11 +879,11 @@ hipError_t launch_train(const cpg_model& model, const uint32_t* packed, const ui
     const int lanes = (int)(C / kLanePos);
     unsigned int* done = reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep);
     if (nchunks >= kEstRepMinChunks)
-        hipLaunchKernelGGL((k_estep_chunk<true, true>), dim3((unsigned)nchunks), dim3(lanes),
+        hipLaunchKernelGGL((k_estep_chunk_rep<true>), dim3((unsigned)nchunks), dim3(lanes),
                            estep_lds(lanes, true), s, model, packed, C, acc, gtab, done, out, sign,
                            cacc, cout);
     else
-        hipLaunchKernelGGL((k_estep_chunk<true, false>), dim3((unsigned)nchunks), dim3(lanes),
+        hipLaunchKernelGGL((k_estep_chunk<true>), dim3((unsigned)nchunks), dim3(lanes),
                            estep_lds(lanes, false), s, model, packed, C, acc, gtab, done, out, sign,
                            cacc, cout);
     return hipGetLastError();

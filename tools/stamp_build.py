@@ -58,6 +58,15 @@ def main():
     subprocess.run(["make", "-s", "-j8", "-C", DST, "OBJDIR=../../obj",
                     f"OUT={os.path.join(R, 'build', 'abl', os.environ.get('STAMP_OUT', 'libcpg_stamp.so'))}", f"CXXFLAGS={base}", os.path.join(R, 'build', 'abl', os.environ.get('STAMP_OUT', 'libcpg_stamp.so'))],
                    check=True)
+    # the package tree that loads it (CPG_DEV_PKG=build/abl/pkg_stamp)
+    pkg = os.path.join(R, "build", "abl", "pkg_" + os.environ.get("STAMP_OUT", "libcpg_stamp.so")[7:-3], "cpgisland_amd")
+    shutil.rmtree(pkg, ignore_errors=True)
+    os.makedirs(pkg)
+    for f in os.listdir(os.path.join(R, "cpgisland_amd")):
+        if f.endswith(".py"):
+            shutil.copy(os.path.join(R, "cpgisland_amd", f), pkg)
+    shutil.copy(os.path.join(R, "build", "abl", os.environ.get("STAMP_OUT", "libcpg_stamp.so")),
+                os.path.join(pkg, "libcpg.so"))
 
 
 if __name__ == "__main__":

@@ -35,5 +35,7 @@ print("median ticks (10 ns):", " ".join(f"{n} {np.median(d[:, i]):.0f}" for i, n
 print("mean ticks   (10 ns):", " ".join(f"{n} {np.mean(d[:, i]):.0f}" for i, n in enumerate(names)))
 t0 = st[:, 0].min()
 print("wg lifetime median", np.median(st[:, 11] - st[:, 0]), "kernel span", st[:, 11].max() - t0)
+# workgroups resident at once per CU: lifetime x workgroups / span / CUs
+print("mean resident workgroups", float(np.sum(st[:, 11] - st[:, 0]) / (st[:, 11].max() - t0)))
 starts = np.sort(st[:, 0] - t0)
 print("start quantiles", [int(x) for x in np.quantile(starts, [0, .1, .3, .36, .37, .5, .7, .73, .74, .9, 1])])
