@@ -509,6 +509,19 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                                &fz, done));
         return CPG_OK;
     }
+    if (islands_fusable(nch, chunk_len)) {
+        // past the tail fusion: the traceback still writes the island tiles (the bases and
+        // signs are not read again), the two resolve passes run after it
+        IslFuse fz;
+        CPG_HIP(islands_tiles(&fz, wsi, ctx->ws[WS_ISL].bytes, nch, chunk_len, first_chunk, d_out,
+                              cap, d_count, ctx->d_status));
+        CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
+                               d_sign_out, d_score, nullptr, ctx->d_status, s,
+                               static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,
+                               &fz, done));
+        CPG_HIP(islands_resolve(d_packed, fz, chunk_len, s));
+        return CPG_OK;
+    }
     CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
                            d_sign_out, d_score, nullptr, ctx->d_status, s,
                            static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,

@@ -238,6 +238,13 @@ hipError_t islands_fuse(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
                         int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
                         int64_t* count, uint32_t* status, unsigned long long* flags,
                         unsigned int* done, const int64_t* base_in = nullptr);
+// the fused decode past kTailFuseMaxChunks chunks: the traceback writes the island tiles
+// (IslFuse with done == null) and islands_resolve places the records after it
+hipError_t islands_tiles(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
+                         int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
+                         int64_t* count, uint32_t* status, const int64_t* base_in = nullptr);
+hipError_t islands_resolve(const uint32_t* packed, const IslFuse& f, int64_t chunk_len,
+                           hipStream_t s);
 // gtab: the model's one-step tables in device memory (est_tables); needed with PART_ACC
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
                         int64_t chunk_len, unsigned long long* acc, double* out,

@@ -218,6 +218,28 @@ hipError_t islands_fuse(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
     return hipSuccess;
 }
 
+// past 256 chunks the fused decode's traceback writes the tiles (kFTW, plain stores: f->done
+// stays null) and islands_resolve runs the two resolve passes after it
+hipError_t islands_tiles(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
+                         int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
+                         int64_t* count, uint32_t* status, const int64_t* base_in) {
+    if (!islands_fusable(nchunks, chunk_len)) return hipErrorInvalidValue;
+    f->ws = carve_isl(ws, nchunks, chunk_len, kFTW);
+    if (f->ws.bytes > ws_bytes) return hipErrorInvalidValue;
+    f->o = IslOut{out, cap, count, base_in, first_chunk, 0u, status, nchunks};
+    f->done = nullptr;
+    return hipSuccess;
+}
+hipError_t islands_resolve(const uint32_t* packed, const IslFuse& f, int64_t chunk_len,
+                           hipStream_t s) {
+    const int64_t nchunks = f.o.nchunks;
+    hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed,
+                       chunk_len, f.ws, f.o);
+    hipLaunchKernelGGL(k_isl_write, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, chunk_len,
+                       f.ws, f.o);
+    return hipGetLastError();
+}
+
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* wsp, size_t ws_bytes,
                           cpg_island* out, int64_t cap, int64_t* count, uint32_t* status,

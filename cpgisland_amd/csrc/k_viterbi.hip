@@ -2024,6 +2024,9 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kK5Wav
 // lanes holding a run boundary write its records — the island tile kernel's work without
 // reading the sign words back.  Records and totals are agent-scope atomic stores: the
 // chunk's last workgroup reads them (k_vit_trace).
+// kAgent: the records are read by another workgroup of this launch (the chunk's resolve in
+// its last workgroup); otherwise by the resolve kernels after it (plain stores).
+template <bool kAgent>
 __device__ __forceinline__ void trace_tile(const uint32_t (&out)[8], const uint32_t (&P)[16],
                                            uint32_t pprev, uint32_t sprev, int64_t k,
                                            const isl::IslWs& tl, int64_t tile) {
@@ -2067,14 +2070,17 @@ __device__ __forceinline__ void trace_tile(const uint32_t (&out)[8], const uint3
         RunRec* cl = tl.closes + tile * tl.cap_t;
 #pragma unroll
         for (int i = 0; i < 8; ++i)
-            emit_word<true>(masks_reg(out[i], i ? out[i - 1] : sprev, P[2 * i], P[2 * i + 1],
-                                i ? P[2 * i - 1] : pprev),
-                      k * 8 + i, e, st, cl);
+            emit_word<kAgent>(masks_reg(out[i], i ? out[i - 1] : sprev, P[2 * i], P[2 * i + 1],
+                                  i ? P[2 * i - 1] : pprev),
+                        k * 8 + i, e, st, cl);
     }
-    if (t == 0) st_cnt5<true>(tl.ttot + tile, tot);
+    if (t == 0) st_cnt5<kAgent>(tl.ttot + tile, tot);
 }
 
-template <bool kIsl>
+// kIsl: 0 = the traceback alone; 1 = + the island tile of its workgroup + the chunk's resolve
+// in the chunk's last workgroup (fused decode, <= 256 chunks); 2 = + the island tile only, the
+// resolve kernels run after it (fused decode past 256 chunks: no re-read of bases and signs)
+template <int kIsl>
 __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __restrict__ bp,
                                                         const uint8_t* __restrict__ endst,
                                                         uint32_t* __restrict__ sign_out,
@@ -2089,7 +2095,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
     if (gid >= g.nchunks * g.nsb) return;
     const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     uint32_t P[16], pprev = 0u;
-    if constexpr (kIsl) {   // the block's 256 bases: issued first, used after the traceback
+    if constexpr (kIsl != 0) {   // the block's 256 bases: issued first, used after the traceback
         const uint32_t* pk = packed + c * (g.C >> 4) + k * 16;
         const uint4* p4 = reinterpret_cast<const uint4*>(pk);
 #pragma unroll
@@ -2152,8 +2158,9 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
         for (int w = 0; w < 8; ++w)
             if (k * 8 + w < nw) so[w] = out[w];
     }
-    if constexpr (kIsl) {
-        trace_tile(out, P, pprev, sb << 31, k, fz.ws, blockIdx.x);
+    if constexpr (kIsl == 2) trace_tile<false>(out, P, pprev, sb << 31, k, fz.ws, blockIdx.x);
+    if constexpr (kIsl == 1) {
+        trace_tile<true>(out, P, pprev, sb << 31, k, fz.ws, blockIdx.x);
         // the chunk's last workgroup to finish resolves it (its records are complete): the
         // island resolve kernel's work, overlapped with the other chunks' tracebacks
         __shared__ int s_last;
@@ -2312,10 +2319,14 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     if (fuse) {   // fused decode: the workgroups are whole island tiles inside one chunk
         if (nsb % kThreads || chunk_len != nsb * kSB || fuse->ws.ntile != nsb / kThreads)
             return hipErrorInvalidValue;
-        hipLaunchKernelGGL(k_vit_trace<true>, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst,
-                           sign_out, status, zero_at, zero_n, packed, *fuse);
+        if (fuse->done)   // the chunk's resolve in its last workgroup
+            hipLaunchKernelGGL(k_vit_trace<1>, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst,
+                               sign_out, status, zero_at, zero_n, packed, *fuse);
+        else              // the tiles only (islands_resolve after it)
+            hipLaunchKernelGGL(k_vit_trace<2>, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst,
+                               sign_out, status, zero_at, zero_n, packed, *fuse);
     } else {
-        hipLaunchKernelGGL(k_vit_trace<false>, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst,
+        hipLaunchKernelGGL(k_vit_trace<0>, dim3(grid), dim3(kThreads), 0, s, g, w.bp, w.endst,
                            sign_out, status, zero_at, zero_n, nullptr, IslFuse{});
     }
     if (degen_out) {
