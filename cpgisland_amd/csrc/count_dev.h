@@ -21,9 +21,13 @@ constexpr uint32_t M55 = 0x55555555u;
 // where v_bfi_b32 issues at half rate (tools/ubench_bits.hip: 2.6 against 4.4 cycles per
 // wave-instruction per SIMD at 4 waves per SIMD)
 __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
+#if defined(__gfx950__)
     uint32_t r;
     asm("v_bitop3_b32 %0, %1, %2, %3 bitop3:0xca" : "=v"(r) : "v"(m), "v"(x), "v"(y));
     return r;
+#else   // (other targets: v_bitop3 is gfx950's; the compiler's v_bfi_b32)
+    return (m & x) | (~m & y);
+#endif
 }
 // 16 bits (bit k) -> even bit positions (bit 2k)
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {

@@ -237,19 +237,20 @@ int cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags) {
     void* p;
     int rc;
     // every slot at its largest over ALL the chunk lengths the decode entry points take
-    // (every multiple of 4096 up to the reference's 1 Mi — a non-power-of-two length takes
+    // (every multiple of 256 up to the reference's 1 Mi — a non-power-of-two length takes
     // another carve): the per-chunk slots (look-back words, done counters) grow with the chunk
     // count, so a reserve for 1 Mi chunks alone would still let a later call with shorter
-    // chunks grow a slot — a device-wide synchronisation (ws_get).  Host arithmetic only.
+    // chunks grow a slot — a device-wide synchronisation (ws_get).  Host arithmetic only
+    // (4,096 lengths).
     size_t vit = 0, isl = 0, agg = 0, per_chunk = 0;
-    for (int64_t C = 4096; C <= CPG_DECODE_CHUNK; C += 4096) {
+    for (int64_t C = 256; C <= CPG_DECODE_CHUNK; C += 256) {
         const int64_t nd = nbases / C + 1;
         vit = std::max(vit, viterbi_ws_bytes(nd, C));
         isl = std::max(isl, islands_ws_bytes(nd, C));
         agg = std::max(agg, viterbi_agg_bytes(nd, C));
         per_chunk = std::max(per_chunk, (size_t)(nd + 1) * 8);
     }
-    const int64_t nt = nbases / 4096 + 1;
+    const int64_t nt = nbases / 256 + 1;
     if ((rc = ws_get(ctx, WS_COUNT, count_ws_bytes(nt), &p))) return rc;
     if ((rc = ws_get(ctx, WS_VIT, vit, &p))) return rc;
     if ((rc = ws_get(ctx, WS_ISL, isl, &p))) return rc;

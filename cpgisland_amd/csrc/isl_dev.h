@@ -113,9 +113,8 @@ struct IslWs {
     int32_t* kept;      // per chunk, maxr: rank*2 | stale_in, or -1
     unsigned long long* flags;   // per chunk: epoch << 32 | kept islands (look-back)
     // the two-pass resolve (separate island kernels: no look-back): per chunk {kept islands,
-    // closed runs}, per chunk and lane {keep/map bits, stale_in | local rank << 1}
+    // closed runs}; per run its kept[] word (stale_in, or -1: filtered out)
     int2* cres;
-    uint2* lanest;
     int64_t ntile;      // tiles per chunk
     int64_t cap_t;      // records per tile and kind
     size_t bytes;
@@ -404,8 +403,15 @@ __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws
     }
     int32_t nkt;
     int32_t rank = wg_scan_sum(nk, sk, nkt);
-    if constexpr (kSplit) {
-        ws.lanest[c * nl + t] = make_uint2(bits, stale0 | ((uint32_t)rank << 1));
+    if constexpr (kSplit) {   // every run's kept[] word for write_runs (cached: from the bits)
+        if (cached) {
+            uint32_t st = stale0;
+            for (int64_t j = 0; j < r1 - r0; ++j) {
+                const uint32_t b = bits >> (4 * j);
+                kept[r0 + j] = ((b >> (2 + st)) & 1u) ? (int32_t)st : -1;
+                st = mapply(b & 3u, st);
+            }
+        }
         if (t == 0) ws.cres[c] = make_int2(nkt, (int32_t)nr);
         return;
     }
@@ -525,10 +531,11 @@ __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C,
 
 // The second pass of the two-pass resolve: chunk c's first record = the kept islands of the
 // chunks before it (a workgroup sum over ws.cres, written by the first pass — an earlier
-// kernel, so no workgroup waits for another), then every lane writes its kept islands from
-// the bits and rank the first pass left (run stats re-read for the kept runs only).
+// kernel, so no workgroup waits for another), then every lane ranks and writes its kept
+// islands from the runs' kept[] words (run stats re-read for the kept runs only).
 __device__ __forceinline__ void write_runs(const uint32_t* packed, int64_t C, const IslWs& ws,
-                                           const IslOut& o, int64_t c, long long* s_part) {
+                                           const IslOut& o, int64_t c, long long* s_part,
+                                           int32_t* sk) {
     const int t = threadIdx.x, nl = blockDim.x, lane = t & 63, wv = t >> 6;
     long long before = 0;
     for (int64_t j = t; j < c; j += nl) before += ws.cres[j].x;
@@ -545,28 +552,21 @@ __device__ __forceinline__ void write_runs(const uint32_t* packed, int64_t C, co
     const int64_t nr = cr.y;
     const int64_t per = (nr + nl - 1) / nl;
     const int64_t r0 = min((int64_t)t * per, nr), r1 = min(r0 + per, nr);
-    const uint2 st = ws.lanest[c * nl + t];
+    const int32_t* kept = ws.kept + c * (C / 2 + 1);
+    int32_t nk = 0;
+    for (int64_t r = r0; r < r1; ++r) nk += kept[r] >= 0;
+    int32_t nkt;
+    const int32_t rank = wg_scan_sum(nk, sk, nkt);   // (uniform: every lane reaches it)
+    if (!nk) return;
     const uint32_t* pk = packed + c * (C / 16);
     const Cnt5* to = ws.toff + c * ws.ntile;
     const int64_t gchunk = o.first_chunk + c;
     const uint32_t cbase = (uint32_t)gchunk * (uint32_t)C;   // chunk*0x100000, Java int
-    int64_t dst = base + (int64_t)(st.y >> 1);
-    if (per <= 8) {
-        uint32_t stale = st.y & 1u;
-        for (int64_t j = 0; j < r1 - r0; ++j) {
-            const uint32_t b = st.x >> (4 * j);
-            if ((b >> (2 + stale)) & 1u)
-                put_island(o, run_stat<false, false>(pk, ws, to, c, r0 + j), stale, dst++, gchunk,
-                           cbase);
-            stale = mapply(b & 3u, stale);
-        }
-    } else {
-        const int32_t* kept = ws.kept + c * (C / 2 + 1);
-        for (int64_t r = r0; r < r1; ++r)
-            if (kept[r] >= 0)
-                put_island(o, run_stat<false, false>(pk, ws, to, c, r), (uint32_t)(kept[r] & 1),
-                           dst++, gchunk, cbase);
-    }
+    int64_t dst = base + rank;
+    for (int64_t r = r0; r < r1; ++r)
+        if (kept[r] >= 0)
+            put_island(o, run_stat<false, false>(pk, ws, to, c, r), (uint32_t)(kept[r] & 1),
+                       dst++, gchunk, cbase);
 }
 
 }  // namespace isl

@@ -66,7 +66,6 @@ IslWs carve_isl(void* base, int64_t nchunks, int64_t C, int64_t tw) {
     w.toff = (Cnt5*)take(nt * sizeof(Cnt5));
     w.kept = (int32_t*)take(nchunks * maxr * 4);
     w.cres = (int2*)take(nchunks * sizeof(int2));
-    w.lanest = (uint2*)take(nchunks * kIT * sizeof(uint2));
     w.flags = nullptr;   // WS_IFLG (the fused decode's look-back)
     w.bytes = o + 256;
     return w;
@@ -188,7 +187,8 @@ __global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int
 __global__ __launch_bounds__(kIT) void k_isl_write(const uint32_t* packed, int64_t C, IslWs ws,
                                                   IslOut o) {
     __shared__ long long s_part[kIT / 64];
-    write_runs(packed, C, ws, o, blockIdx.x, s_part);
+    __shared__ int32_t sk[kIT / 64];
+    write_runs(packed, C, ws, o, blockIdx.x, s_part, sk);
 }
 
 }  // namespace

@@ -106,7 +106,7 @@ void        cpg_close(cpg_ctx* ctx);
 const char* cpg_last_error(void);
 int         cpg_abi_version(void);
 /* Pre-size the context's workspace for inputs of up to nbases bases, for every chunk length
- * the exact-scan entry points take (every multiple of 4096 up to 1 Mi), so that the _d entry
+ * the exact-scan entry points take (every multiple of 256 up to 1 Mi), so that the _d entry
  * points never allocate (required before hipGraph capture).  A slot that has to grow later (a
  * larger input) synchronises the whole device first: the old buffer may still be read by a
  * kernel on another stream.

@@ -172,9 +172,10 @@ def test_reserved_general_path_does_not_allocate(dev):
     try:
         ctx.reserve(n, general=True)
         before = ctx.workspace_bytes()
-        for C in (4096, 65536, 12288):
+        for C in (4096, 65536, 12288, 768, 12544):   # (multiples of 256 too)
             D.viterbi(ctx, HmmModel.from_struct(mg), dp, n, C)
             D.viterbi(ctx, HmmModel.initial(), dp, n, C)
+            D.decode(ctx, HmmModel.initial(), dp, n, C)
         st, sc = D.viterbi_states(ctx, HmmModel.from_struct(mg), dp, n, n)   # one chunk
         torch.cuda.synchronize()
         ctx.sync()
