@@ -40,8 +40,15 @@ HBM_PEAK_GBS = 8000.0          # MI355X_MICROARCH.md: 8.0 TB/s spec
 # lane products 4 two-by-two products per 16 positions = 3 — implementation recomputation
 # (the second forward pass over half of each mini-block) not counted
 FP64_PEAK_TFLOPS = 78.6
-# the training pass's kernel (the E-step chunk kernel; its kCnt instantiation in the fused pass)
+# the training pass's kernel (the E-step chunk kernel; its kCnt instantiation in the fused pass);
+# launches of >= 2,048 chunks run its lane-private-rows form (k_estep.hip, k_estep_chunk_rep)
 ESTEP_KERNEL = "k_estep_chunk"
+ESTEP_KERNEL_REP = "k_estep_chunk_rep"
+EST_REP_MIN_CHUNKS = 2048
+
+
+def estep_kernel(nbases):
+    return ESTEP_KERNEL_REP if nbases // TRAIN >= EST_REP_MIN_CHUNKS else ESTEP_KERNEL
 ESTEP_FLOPS_PER_BASE = 23
 # algorithmic bytes per base of each phase: the fused
 # decode (cpg_decode_d) reads the packed bases once and writes the 1-bit path (0.375); the
@@ -621,7 +628,7 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
                           "islands_found": sum(counts)},
                "phases_ms": {"train_pass": round(tr_ms, 4)},
                "host_issue_ms_per_step": round(issue * 1e3 / args.steps, 4),
-               "roofline": {"bound": "hbm", "kernel": ESTEP_KERNEL, "phase": "train_pass",
+               "roofline": {"bound": "hbm", "kernel": estep_kernel(tr_n), "phase": "train_pass",
                             "achieved": round(ach, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                             "frac": round(ach / HBM_PEAK_GBS, 4), "traffic": None,
                             "algorithmic_bytes": bpb * tr_n, "bytes_per_base": bpb},
@@ -632,7 +639,7 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
                "fingerprint": fp, "bw_iteration": bw}
         # HBM traffic of the training pass at this rank's size: the PMC profile of the C3
         # workload on one GPU (tools/pmc.sh c3), scaled to the shard's bases
-        pmc = _pmc_traffic(ESTEP_KERNEL, tr_n, name="pmc_c3.json", scale=True)
+        pmc = _pmc_traffic(estep_kernel(tr_n), tr_n, name="pmc_c3.json", scale=True)
         if pmc:
             out["roofline"]["traffic"] = pmc["traffic_bytes"]
             out["roofline"]["traffic_source"] = "stored PMC profile, not this run: " + pmc["source"]

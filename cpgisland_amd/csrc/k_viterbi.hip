@@ -1766,6 +1766,13 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
         return k + 1 == g.nsb ? ent[g.nsb] : went[sgi + 1];
     };
     const double2 v0 = entries(false);   // this block's entry
+    // the next block's entry (the self-check below) is the next lane's own entry, the same
+    // computation (entries(true) == its entries(false)): taken from it through LDS (same wave:
+    // its LDS accesses complete in order; nothing held in registers across the walk), not
+    // loaded again — except by the wave's last lane and a chunk's last block
+    __shared__ double2 s_v0[kThreads];
+    s_v0[threadIdx.x] = v0;
+    const bool vn_here = (threadIdx.x & 63) != 63 && k + 1 < g.nsb;
     double P = v0.x, M = v0.y;
     uint32_t oP = 1u, oM = 0u;   // origin sign of the current '+' / '-' survivor
     uint32_t wP0 = 0, wP1 = 0, wM0 = 0, wM1 = 0;
@@ -1855,7 +1862,8 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
             }
         }
     }
-    const double2 nx = entries(true);   // the next block's entry: the self-check
+    asm volatile("" ::: "memory");   // (the read stays after the walk and the write)
+    const double2 nx = vn_here ? s_v0[threadIdx.x + 1] : entries(true);   // the self-check
     if (__double_as_longlong(nx.x) != __double_as_longlong(P) ||
         __double_as_longlong(nx.y) != __double_as_longlong(M))
         atomicOr(status, ST_VERIFY_ENTRY);
