@@ -340,11 +340,7 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
     double2* RA = reinterpret_cast<double2*>(reinterpret_cast<unsigned char*>(fck) +
                                              (size_t)(kLanePos / 16) * nl * sizeof(double2));
     double2* RB = RA + kKeys * 16;
-    if (kRep)
-        for (int i = t; i < kKeys * 16; i += nl) {
-            RA[i] = gtab[32 + (i >> 4)];
-            RB[i] = gtab[32 + kKeys + (i >> 4)];
-        }
+    // (kRep: the lane-private row copy is made by waves 1.. while wave 0 walks the rows, 2c)
     const double2* __restrict__ rA = RA + (t & 15);   // this lane's column of the copy
     const double2* __restrict__ rB = RB + (t & 15);
     const Codes cd0 = lane_codes(pk, t);   // (in flight across the barrier)
@@ -355,12 +351,16 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
     uint32_t sgp = 0u;
     if (kCnt) {
         if (t < cnt::kRaw) scnt[t] = 0u;
-        const uint32_t* sk = sign + c * (C / 32);
-        sg = *reinterpret_cast<const uint2*>(sk + 2 * t);
-        sgp = sk[t > 0 ? 2 * t - 1 : 0];   // (unconditional; its sign bit taken at use)
+        if (t < 64) {   // wave 0's label words (the other waves load theirs in 2c)
+            const uint32_t* sk = sign + c * (C / 32);
+            sg = *reinterpret_cast<const uint2*>(sk + 2 * t);
+            sgp = sk[t > 0 ? 2 * t - 1 : 0];   // (unconditional; its sign bit taken at use)
+        }
     }
     __syncthreads();
-    if (kCnt) {   // the lane's 64 bases = one count block (its first is the chunk's first)
+    // the lane's 64 bases = one count block (its first is the chunk's first).  Wave 0 counts
+    // here; the other waves count while wave 0 walks the rows (2c), where they would wait
+    if (kCnt && t < 64) {
         __builtin_amdgcn_sched_barrier(0);   // kept apart from phase 1: registers
         if (t == 0) atomicAdd(&scnt[64 + cnt::init_state(cd0.raw[0], sg.x)], 1u);
         cnt::Lane lc;
@@ -511,6 +511,25 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
                 }
             // the chunk log-likelihood from the last group's alpha after all rows
             if (g == 15) *sLL = log(vP + vM) + (double)E * 0.69314718055994530942;
+        }
+    } else {
+        // waves 1..: work that would otherwise sit in the prologue's critical path —
+        // the lane-private row copy (kRep) and the labelled counts of their blocks (kCnt,
+        // the words reloaded: nothing kept live across the scans)
+        if (kRep)
+            for (int i = t - 64; i < kKeys * 16; i += nl - 64) {
+                RA[i] = gtab[32 + (i >> 4)];
+                RB[i] = gtab[32 + kKeys + (i >> 4)];
+            }
+        if (kCnt) {
+            const uint4 w = *reinterpret_cast<const uint4*>(pk + 4 * t);
+            const uint32_t wp = pk[4 * t - 1];
+            const uint32_t* sk = sign + c * (C / 32);
+            const uint2 sw = *reinterpret_cast<const uint2*>(sk + 2 * t);
+            const uint32_t swp = sk[2 * t - 1];
+            cnt::Lane lc;
+            lc.block(w, sw, wp, swp >> 31, false, scnt);
+            lc.flush(scnt);
         }
     }
     __syncthreads();
