@@ -114,6 +114,24 @@ __device__ __forceinline__ void reset_done(unsigned int* done) {
 __device__ __forceinline__ unsigned long long load_agent(const unsigned long long* p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
+// The E-step's 128-bit fixed-point accumulators (k_estep.hip, k_contigs.hip) as SPLIT sums:
+// a slot pair (w0, w1) accumulates the low 32 bits of each addend in w0 and the rest (the
+// addend >> 32, two's complement) in w1, so the value is w1 * 2^32 + w0 — two non-returning
+// 64-bit atomics per addend, no carry to wait for (a returning atomic's round trip had been
+// most of the E-step's epilogue).  No overflow: w0 gains < 2^32 per addend (< 2^48 for 2^16
+// addends per replica), |w1| < 2^63 for sums below 2^95.  acc_sum128 is the finalize's side.
+__device__ __forceinline__ void acc_split_add(unsigned long long* w, unsigned long long lo,
+                                              unsigned long long hi) {   // addend = hi 2^64 + lo
+    const unsigned long long p0 = lo & 0xFFFFFFFFull, p1 = (lo >> 32) | (hi << 32);
+    if (p0) atomicAdd(w, p0);
+    if (p1) atomicAdd(w + 1, p1);
+}
+// sum of (w0, w1) pairs, as a 128-bit two's complement value (lo, hi)
+__device__ __forceinline__ void acc_sum128(unsigned long long s0, unsigned long long s1,
+                                           unsigned long long& lo, unsigned long long& hi) {
+    lo = (s1 << 32) + s0;
+    hi = (unsigned long long)((long long)s1 >> 32) + (lo < s0 ? 1ull : 0ull);
+}
 #endif
 
 // ---- context -----------------------------------------------------------------------

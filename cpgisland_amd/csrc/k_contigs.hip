@@ -287,12 +287,11 @@ __device__ __forceinline__ int vnorm(double& x, double& y) {
     }
     return k;
 }
-// 128-bit two's-complement accumulation (lo, hi) with 64-bit atomics and carry
+// a 128-bit addend (lo, hi) into the E-step's split accumulators (acc_split_add,
+// cpg_internal.h; finalized by k_estep_final)
 __device__ __forceinline__ void acc128_add2(unsigned long long* lohi, unsigned long long lo,
                                             unsigned long long hi) {
-    const unsigned long long old = atomicAdd(lohi, lo);
-    hi += (old + lo < old) ? 1ull : 0ull;
-    if (hi) atomicAdd(lohi + 1, hi);
+    acc_split_add(lohi, lo, hi);
 }
 
 constexpr int kCtgEstWaves = 3;   // min waves per SIMD (VGPR budget 512 / this; 2..4 measured)

@@ -200,13 +200,11 @@ __device__ __forceinline__ unsigned long long to_fixed_init(double y47) {   // y
     return __double2ull_rn(ldexp(y47, 15));
 }
 
-// 128-bit two's-complement accumulation with 64-bit atomics: the adder that wraps the low
-// word carries into the high word (plus the sign extension of a negative addend)
+// a 64-bit addend (sign-extended when negative) into a split 128-bit accumulator
+// (acc_split_add, cpg_internal.h)
 __device__ __forceinline__ void acc128_add(unsigned long long* lohi, unsigned long long v,
                                            bool negative) {
-    const unsigned long long old = atomicAdd(lohi, v);
-    const unsigned long long hi = (negative ? ~0ull : 0ull) + (old + v < old ? 1ull : 0ull);
-    if (hi) atomicAdd(lohi + 1, hi);
+    acc_split_add(lohi, v, negative ? ~0ull : 0ull);
 }
 
 // the lane's 64 dinucleotide codes (prev | cur << 2), 8 per word, read once from HBM
@@ -754,15 +752,14 @@ __device__ void finalize(const cpg_model& model, unsigned long long* acc, double
                          double* out) {
     const int t = threadIdx.x;
     for (int i = t; i < kSlab; i += blockDim.x) {
-        unsigned long long lo = 0ull, hi = 0ull;   // 128-bit sum of the replicas
+        unsigned long long s0 = 0ull, s1 = 0ull;   // the replicas' split sums
         for (int r = 0; r < kAccRep; ++r) {
             const unsigned long long* a = acc + 2 * (r * kSlab + i);
-            const unsigned long long l = kAgent ? load_agent(a) : a[0];
-            const unsigned long long h = kAgent ? load_agent(a + 1) : a[1];
-            const unsigned long long nl = lo + l;
-            hi += h + (nl < lo ? 1ull : 0ull);
-            lo = nl;
+            s0 += kAgent ? load_agent(a) : a[0];
+            s1 += kAgent ? load_agent(a + 1) : a[1];
         }
+        unsigned long long lo, hi;   // 128-bit value
+        acc_sum128(s0, s1, lo, hi);
         const bool neg = (long long)hi < 0;   // only the log-likelihood row can be negative
         if (neg) {                             // magnitude first: no cancellation
             lo = ~lo + 1ull;
