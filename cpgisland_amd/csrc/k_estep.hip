@@ -296,6 +296,11 @@ constexpr int kWavesPerEURep = CPG_EST_WPE_REP;
 #ifndef CPG_EST_PFD_REP
 #define CPG_EST_PFD_REP 1
 #endif
+// blocks (two positions each) between the alpha renormalisations of the main loop (2: every
+// 4 positions; a build-time override for measurement builds)
+#ifndef CPG_EST_RNB
+#define CPG_EST_RNB 2
+#endif
 // kCnt: the fused training pass — each lane also counts its 64 bases' labelled transitions
 // (count_dev.h; sign = the label bits), added into the count accumulators cacc, and the last
 // workgroup finalizes both (cout: cpg_counts_i64).  Needs >= 256 lanes (chunks >= 16 Ki).
@@ -455,65 +460,51 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
     const double fa = model.pi[o0], fb = model.pi[o0 + 4];   // alpha_0 (b = 1 when live)
     __syncthreads();
     if (t < 64) {
-        // lane g < 16: rows 4g .. 4g+3 (rows past nr: identity)
-        const int g = t & 15;
-        Mat gp = mid();
+        // lane r: row r (rows past nr: identity).  Inclusive prefix and suffix products of the
+        // 64 row totals — DPP inside 16-lane rows, then two cross-row levels by shuffles —
+        // give alpha entering and beta leaving every row as ONE mat-vec each (round 5: the
+        // walk of 4 rows per lane by 16 lanes had been a chain of 4 + 4 dependent steps)
+        const int r = t;
+        const Mat x = r < nr ? sRP[r] : mid();
+        Mat xp = x, xs = x;
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
-            if (4 * g + j < nr) gp = mmul_nn(gp, sRP[4 * g + j]);
-        mnorm(gp);
-        Mat xg = gp, yg = gp;
-#pragma unroll
-        for (int off = 1; off < 16; off <<= 1) {   // the 16 group totals: DPP scans
-            const Mat yp = row_up(xg, off), ys = row_down(yg, off);
-            xg = off < 8 ? mmul_nn(yp, xg) : mmul(yp, xg);
-            yg = off < 8 ? mmul_nn(yg, ys) : mmul(yg, ys);
+        for (int off = 1; off < 16; off <<= 1) {
+            const Mat yp = row_up(xp, off), ys = row_down(xs, off);
+            xp = off < 8 ? mmul_nn(yp, xp) : mmul(yp, xp);
+            xs = off < 8 ? mmul_nn(xs, ys) : mmul(xs, ys);
         }
-        const Mat ep = row_up(xg, 1), es = row_down(yg, 1);   // groups before / after g
-        // alpha entering group g (alpha_0 x the groups before), then its rows in order
+#pragma unroll
+        for (int off = 16; off < 64; off <<= 1) {   // across the 16-lane rows
+            Mat yp = shfl_up_mat(xp, off), ys = shfl_down_mat(xs, off);
+            if (r < off) yp = mid();
+            if (r + off >= 64) ys = mid();
+            xp = mmul(yp, xp);
+            xs = mmul(xs, ys);
+        }
+        Mat ep = shfl_up_mat(xp, 1), es = shfl_down_mat(xs, 1);   // rows before / after r
+        if (r == 0) ep = mid();
+        if (r == 63) es = mid();
+        // alpha entering row r: alpha_0 x the rows before; beta leaving it: the rows after x 1
         double vP = fa * ep.a + fb * ep.c, vM = fa * ep.b + fb * ep.d;
-        int E = ep.e + vnorm(vP, vM);
-        double uP = es.a + es.b, uM = es.c + es.d;   // beta leaving group g (unit at the end)
+        vnorm(vP, vM);
+        double uP = es.a + es.b, uM = es.c + es.d;
         vnorm(uP, uM);
-        double2 av[4], bv[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {   // rows 4g + j, forward
-            av[j] = make_double2(vP, vM);
-            const int r = 4 * g + j;
-            if (r < nr) {
-                const Mat R = sRP[r];
-                const double nP = vP * R.a + vM * R.c, nM = vP * R.b + vM * R.d;
-                vP = nP;
-                vM = nM;
-                E += R.e + vnorm(vP, vM);
-            }
+        if (r < nr) {
+            sAR[r] = make_double2(vP, vM);
+            sBR[r] = make_double2(uP, uM);
         }
-#pragma unroll
-        for (int j = 3; j >= 0; --j) {   // rows 4g + j, backward
-            bv[j] = make_double2(uP, uM);
-            const int r = 4 * g + j;
-            if (r < nr) {
-                const Mat R = sRP[r];
-                const double nP = R.a * uP + R.b * uM, nM = R.c * uP + R.d * uM;
-                uP = nP;
-                uM = nM;
-                vnorm(uP, uM);
-            }
-        }
-        if (t < 16) {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-                if (4 * g + j < nr) {
-                    sAR[4 * g + j] = av[j];
-                    sBR[4 * g + j] = bv[j];
-                }
-            // the chunk log-likelihood from the last group's alpha after all rows
-            if (g == 15) *sLL = log(vP + vM) + (double)E * 0.69314718055994530942;
+        if (r == 63) {   // the chunk log-likelihood: alpha_0 x all rows (lane 63's inclusive)
+            double aP = fa * xp.a + fb * xp.c, aM = fa * xp.b + fb * xp.d;
+            const int k = vnorm(aP, aM);
+            *sLL = log(aP + aM) + (double)(xp.e + k) * 0.69314718055994530942;
         }
     } else {
         // waves 1..: work that would otherwise sit in the prologue's critical path —
         // the lane-private row copy (kRep) and the labelled counts of their blocks (kCnt,
         // the words reloaded: nothing kept live across the scans)
+        // every lane is past its 4-step table reads (phase 1, before the barrier above): the
+        // union becomes the bins
+        for (int i = t - 64; i < kKeyRows * 16; i += nl - 64) bins[i] = 0ull;
         if (kRep)
             for (int i = t - 64; i < kKeys * 16; i += nl - 64) {
                 RA[i] = gtab[32 + (i >> 4)];
@@ -531,9 +522,10 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
         }
     }
     __syncthreads();
-    // every lane is past its 4-step table reads (phase 1, before the barrier above): the
-    // union becomes the bins, zeroed here, ready at the checkpoints' barrier
-    for (int i = t; i < kKeyRows * 16; i += nl) bins[i] = 0ull;
+    // the union has become the bins: zeroed by waves 1.. during the walk (2c), or here by the
+    // only wave (its own LDS accesses stay in order: no barrier before the main loop either)
+    if (nl == 64)
+        for (int i = t; i < kKeyRows * 16; i += nl) bins[i] = 0ull;
     unsigned long long* racc = acc + 2 * kSlab * (c % kAccRep);
     if (t == nl - 1) {   // the chunk log-likelihood, in signed 2^-24 units (added now: nothing
                          // stays live across the main loop)
@@ -565,7 +557,8 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
         fck[m * nl + t] = make_double2(xP, xM);
     }
     fck[t] = make_double2(aP, aM);
-    __syncthreads();
+    // (no barrier: a lane reads only its own checkpoints; the bins were zeroed before the
+    // walk's barrier)
 
     // 3a. (bins zeroed above) alpha entering mini-block m = alpha entering the lane times
     //     phase 1's product of the first m mini-blocks (any per-position scale cancels in the
@@ -605,7 +598,10 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
         const double2 f = fck[m * nl + t];   // alpha at the position before the mini-block
         constexpr int kB = kMB / 2;          // blocks per mini-block
         double alP[kB], alM[kB];
-        int kf[kB / 2];   // alpha's power-of-two shifts at positions 3, 7, 11, 15 (A_2,4,6,8)
+        // alpha renormalised after every kRNB blocks (2: positions 3, 7, 11, 15, i.e. A_2, A_4,
+        // A_6, A_8); kf = the power-of-two shifts applied there
+        constexpr int kRNB = CPG_EST_RNB;
+        int kf[kB / kRNB];
         double xP = f.x, xM = f.y;
         // the rows are issued kFPD steps ahead (the scheduling barrier keeps them there: the
         // compiler had waited for each step's reads right before using them, one LDS round
@@ -630,12 +626,12 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
             const double nP = xP * ma.x + xM * mb.x, nM = xP * ma.y + xM * mb.y;
             xP = nP;
             xM = nM;
-            if (j & 1) kf[j >> 1] = vnorm(xP, xM);
+            if ((j + 1) % kRNB == 0) kf[(j + 1) / kRNB - 1] = vnorm(xP, xM);
         }
         // y_15 = beta_15 * 2^{47 - s_15} / (A_8 . beta_15)  (A_8 = alpha_15 after its shift)
         vnorm(yP, yM);
         {
-            const double r = ldexp(rcp_nr(xP * yP + xM * yM), 47 - kf[kB / 2 - 1]);
+            const double r = ldexp(rcp_nr(xP * yP + xM * yM), 47 - kf[kB / kRNB - 1]);
             yP *= r;
             yM *= r;
         }
@@ -680,9 +676,9 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
             }
             yP = t00 + t01;
             yM = t10 + t11;
-            if (j == 2 || j == 4 || j == 6) {   // crossing A_j's renormalisation point
-                yP = ldexp(yP, -kf[j / 2 - 1]);
-                yM = ldexp(yM, -kf[j / 2 - 1]);
+            if (j > 0 && j % kRNB == 0) {   // crossing A_j's renormalisation point
+                yP = ldexp(yP, -kf[j / kRNB - 1]);
+                yM = ldexp(yM, -kf[j / kRNB - 1]);
             }
         }
     }
@@ -694,16 +690,31 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
     // chunk totals: row te = key * 4 + (2a + c), the sum of its 16 columns (integer: exact in
     // any order); the key's 4 raw sums (lanes 4 key .. 4 key + 3 of one wave) -> its block
     // count -> K removed -> the key accumulators (slots kSlabCls + row)
-    for (int r = te; r < kKeyRows; r += nl) {   // (nl: a multiple of 64)
-        const unsigned long long* row = bins + r * 16;
+    if (nl == 4 * kKeyRows) {   // the reference's chunk: 4 lanes per row, 4 columns each
+        const int r = te >> 2, q = te & 3;
+        const unsigned long long* row = bins + r * 16 + 4 * q;
         unsigned long long s = 0;
 #pragma unroll
-        for (int col = 0; col < 16; ++col) s += row[(col + r) & 15];   // rotated: no conflicts
+        for (int i = 0; i < 4; ++i) s += row[(i + r) & 3];   // rotated: 16 lanes, 16 columns
+        s += xor_te(s, te, 1);   // the row's sum (lane addresses from te, see above)
+        s += xor_te(s, te, 2);
         unsigned long long S = s;
-        S += xor_te(S, te, 1);   // (lane addresses from te, see above)
-        S += xor_te(S, te, 2);
+        S += xor_te(S, te, 4);   // the key's 4 rows
+        S += xor_te(S, te, 8);
         s -= class_count(S) * kMagicBits;
-        if (s) acc128_add(racc + 2 * (kSlabCls + r), s, false);
+        if (q == 0 && s) acc128_add(racc + 2 * (kSlabCls + r), s, false);
+    } else {
+        for (int r = te; r < kKeyRows; r += nl) {   // (nl: a multiple of 64)
+            const unsigned long long* row = bins + r * 16;
+            unsigned long long s = 0;
+#pragma unroll
+            for (int col = 0; col < 16; ++col) s += row[(col + r) & 15];   // rotated: no conflicts
+            unsigned long long S = s;
+            S += xor_te(S, te, 1);   // (lane addresses from te, see above)
+            S += xor_te(S, te, 2);
+            s -= class_count(S) * kMagicBits;
+            if (s) acc128_add(racc + 2 * (kSlabCls + r), s, false);
+        }
     }
     if (kCnt && te < cnt::kRaw) {   // the count sums (kCnt: >= 256 lanes)
         const uint32_t v = cnt::raw_of(scnt, te);
@@ -809,6 +820,22 @@ __global__ __launch_bounds__(256) void k_estep_final(const cpg_model model,
     finalize<false>(model, acc, vsum, out);
 }
 
+// The long launches' finalize as its own one-workgroup launch (both outputs of a training
+// pass): the chunk kernel then skips the last-workgroup protocol — the wait for every one of
+// its atomics, two barriers and a returning device-scope atomic per workgroup (0.7 us of a
+// workgroup's ~27, stamped) — for one launch per call.
+__global__ __launch_bounds__(256) void k_train_final(const cpg_model model,
+                                                     unsigned long long* __restrict__ acc,
+                                                     double* __restrict__ out,
+                                                     unsigned long long* __restrict__ cacc,
+                                                     int64_t* __restrict__ cout) {
+    __shared__ double vsum[kSlab];
+    __shared__ uint64_t craw[cnt::kRaw];
+    if (cacc && threadIdx.x < cnt::kRaw) cnt::fin_load<false>(cacc, craw, threadIdx.x);
+    finalize<false>(model, acc, vsum, out);   // (its barriers order craw too)
+    if (cacc) cnt::fin_store(cacc, craw, cout, threadIdx.x, blockDim.x);
+}
+
 // cpg_counts_f64 from the 73 sums: init[8] trans[8][8] emit[8][4] loglik; thread t < 105
 __device__ void final_estep(const double* v, int t, double* __restrict__ out) {
     double r = 0.0;
@@ -853,6 +880,12 @@ size_t estep_lds(int lanes, bool rep) {   // the union is sized for 16 waves; fe
 #define CPG_EST_REP_MIN 2048
 #endif
 constexpr int64_t kEstRepMinChunks = CPG_EST_REP_MIN;
+// from this many chunks the finalize runs as its own launch (k_train_final): a launch costs
+// ~2-4 us, the last-workgroup protocol ~0.7 us per round of workgroups
+#ifndef CPG_EST_SEPFIN_MIN   // (a build-time override for measurement builds only)
+#define CPG_EST_SEPFIN_MIN 2048
+#endif
+constexpr int64_t kEstSepFinMinChunks = CPG_EST_SEPFIN_MIN;
 }  // namespace
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
@@ -864,8 +897,9 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
     if ((parts & PART_ACC) && nchunks > 0) {
         const int lanes = (int)(C / kLanePos);
         if (!gtab) return hipErrorInvalidValue;   // est_tables
-        unsigned int* done =
-            parts == PART_ALL ? reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep) : nullptr;
+        const bool sepfin = parts == PART_ALL && nchunks >= kEstSepFinMinChunks;
+        unsigned int* done = parts == PART_ALL && !sepfin
+                                 ? reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep) : nullptr;
         if (nchunks >= kEstRepMinChunks)
             hipLaunchKernelGGL((k_estep_chunk_rep<false>), dim3((unsigned)nchunks), dim3(lanes),
                                estep_lds(lanes, true), s, model, packed, C, acc, gtab, done, out,
@@ -874,6 +908,11 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
             hipLaunchKernelGGL((k_estep_chunk<false>), dim3((unsigned)nchunks), dim3(lanes),
                                estep_lds(lanes, false), s, model, packed, C, acc, gtab, done, out,
                                nullptr, nullptr, nullptr);
+        if (sepfin) {
+            hipLaunchKernelGGL(k_train_final, dim3(1), dim3(256), 0, s, model, acc, out, nullptr,
+                               nullptr);
+            return hipGetLastError();
+        }
         if (done) return hipGetLastError();
     }
     if (parts & PART_FINAL)
@@ -893,7 +932,9 @@ hipError_t launch_train(const cpg_model& model, const uint32_t* packed, const ui
         return e != hipSuccess ? e : hipMemsetAsync(cout, 0, 124 * sizeof(int64_t), s);
     }
     const int lanes = (int)(C / kLanePos);
-    unsigned int* done = reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep);
+    const bool sepfin = nchunks >= kEstSepFinMinChunks;
+    unsigned int* done =
+        sepfin ? nullptr : reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep);
     if (nchunks >= kEstRepMinChunks)
         hipLaunchKernelGGL((k_estep_chunk_rep<true>), dim3((unsigned)nchunks), dim3(lanes),
                            estep_lds(lanes, true), s, model, packed, C, acc, gtab, done, out, sign,
@@ -902,6 +943,8 @@ hipError_t launch_train(const cpg_model& model, const uint32_t* packed, const ui
         hipLaunchKernelGGL((k_estep_chunk<true>), dim3((unsigned)nchunks), dim3(lanes),
                            estep_lds(lanes, false), s, model, packed, C, acc, gtab, done, out, sign,
                            cacc, cout);
+    if (sepfin)
+        hipLaunchKernelGGL(k_train_final, dim3(1), dim3(256), 0, s, model, acc, out, cacc, cout);
     return hipGetLastError();
 }
 

@@ -149,6 +149,11 @@ int cpg_initial_model(cpg_model* out);
  *           compat_quirks != 0 returns CPG_E_REF_CRASH when the reference would call
  *           observedSequence.get(i) on an empty list (:257-258); *nbases then holds
  *           the bases decoded before the crash.
+ * The base count is a Java int (:107, :236): at 2^32 bases it wraps to 0 and the chunk test
+ * is skipped.  Mode 1 then decodes the held chunk at the next multiple and drops the 2^20
+ * bases read after the wrap (no error: the reference's clear()); mode 0 returns
+ * CPG_E_REF_CRASH at the byte that brings the count to 2^32 + 65,536 (DenseVector.set past
+ * its size, :133-134) — whatever compat_quirks says.
  * packed: caller buffer of cap_bases/16 words; *nbases = bases written. */
 int cpg_ingest(const char* txt, size_t n, int mode, int compat_quirks,
                uint32_t* packed, int64_t cap_bases, int64_t* nbases);
