@@ -1698,6 +1698,25 @@ __device__ __forceinline__ uint32_t push_bit(uint32_t w, bool c) {
     return r;
 }
 
+// nibble m (compile-time, 0..7) of w times 16 in one VALU op: SDWA byte selects — a low
+// nibble shifted into a byte whose other bits are dropped, a high nibble masked in place
+// (the shift + mask pair they replace was two ops per step of K5's walk)
+__device__ __forceinline__ uint32_t nib16(uint32_t w, int m) {
+    uint32_t r;
+    const uint32_t f0 = 0xF0u;
+    switch (m) {
+        case 0: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_0" : "=v"(r) : "v"(w)); break;
+        case 1: r = w & 0xF0u; break;
+        case 2: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(w)); break;
+        case 3: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_1" : "=v"(r) : "v"(f0), "v"(w)); break;
+        case 4: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(w)); break;
+        case 5: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_2" : "=v"(r) : "v"(f0), "v"(w)); break;
+        case 6: asm("v_lshlrev_b32_sdwa %0, 4, %1 dst_sel:BYTE_0 dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(w)); break;
+        default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(f0), "v"(w)); break;
+    }
+    return r;
+}
+
 // origin map (bit x = origin sign of the state-x survivor, '+' = 1) of 64 steps from their
 // backpointer bits (bit j of bP / bM: step j's '+' / '-' survivor came from '-'): step j maps
 // its state to the previous one, b_j(1) = !bP_j, b_j(0) = !bM_j, and the quad's map is
@@ -1800,13 +1819,22 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
         // quads of 64 steps; the ring of kLook lookups in flight runs across quad borders
         // (2 deep: at the 64-VGPR budget, 4 had spilled more and measured slower)
         constexpr int kLook = 2;
-        auto fetch = [&](uint32_t d) { return C64{LA[d].x, LA[d].y, LB[d].x, LB[d].y}; };
+        const unsigned char* LAb = reinterpret_cast<const unsigned char*>(LA);
+        const unsigned char* LBb = reinterpret_cast<const unsigned char*>(LB);
+        auto fetch = [&](uint32_t a) {   // a = code * 16 (byte offset of the entry)
+            const double2 x = *reinterpret_cast<const double2*>(LAb + a);
+            const double2 y = *reinterpret_cast<const double2*>(LBb + a);
+            return C64{x.x, x.y, y.x, y.y};
+        };
+        // step j's code (bases j-1, j) times 16, one VALU op per step: odd i = 2m + 1 is
+        // nibble m of the word, even i = 2m nibble m of the word shifted in by one base
+        // (one alignbit per word)
         auto code = [](const uint4 w, uint32_t prev, int j) {   // j compile-time, < 64
             const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
             const int r = j >> 4, i = j & 15;
             const uint32_t lo = r == 0 ? prev : ww[r - 1];
-            return i == 0 ? (__builtin_amdgcn_alignbit(ww[r], lo, 30) & 15u)
-                          : ((ww[r] >> (2 * i - 2)) & 15u);
+            return (i & 1) ? nib16(ww[r], i >> 1)
+                           : nib16(__builtin_amdgcn_alignbit(ww[r], lo, 30), i >> 1);
         };
         const int64_t wbase = k * kSBWords;
         uint32_t prev = k > 0 ? pk[wbase - 1] : 0u;
@@ -1814,14 +1842,14 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
         C64 ring[kLook];
 #pragma unroll
         for (int j = 0; j < kLook; ++j)
-            ring[j] = fetch((j == 0 && k == 0) ? 16u : code(cur, prev, j));
+            ring[j] = fetch((j == 0 && k == 0) ? 16u * 16u : code(cur, prev, j));
         uint32_t omap = 0x2u;   // identity
 #pragma unroll 1
         for (int q = 0; q < 4; ++q) {
             const uint4 nxt = *reinterpret_cast<const uint4*>(pk + wbase + 4 * (q < 3 ? q + 1 : q));
             // bits pushed in at the bottom: step jj ends at bit 31 - (jj mod 32), reversed below
             uint32_t aP0 = 0, aP1 = 0, aM0 = 0, aM1 = 0;
-#pragma unroll
+#pragma clang loop unroll(full)
             for (int jj = 0; jj < 64; ++jj) {
                 const C64 l = ring[jj % kLook];
                 const int j2 = jj + kLook;   // past the block's end (q == 3): harmless lookups
