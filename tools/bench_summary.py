@@ -8,8 +8,8 @@ print("value", round(d["value"] / 1e9, 1), "Gbase/s", "ms/step", round(d["ms_per
 for k in ("c3_single_gpu", "bw_iteration"):
     if isinstance(d.get(k), dict):
         v = d[k]
-        print(k, {x: v[x] for x in ("value", "ms_per_step", "phases_ms", "ms", "records_sha256",
-                                      "counts_sha256") if x in v})
+        print(k, {x: v[x] for x in ("value", "ms_per_step", "phases_ms", "ms_per_iteration",
+                                      "decode_ms", "fingerprint") if x in v})
 for k in ("roofline", "roofline_count", "roofline_decode"):
     if isinstance(d.get(k), dict):
         v = d[k]

@@ -1,8 +1,8 @@
 #!/bin/bash
-# Round 5: the gpu suite + smoke + driver bench (tools/gpu_check.sh), then the 2-rank gloo
+# Round-end check: the gpu suite + smoke + driver bench (tools/gpu_check.sh), then the 2-rank gloo
 # rehearsal on this one GPU (bench.py's own launcher, both ranks' decodes concurrent) whose
 # C3 fingerprints must equal the N = 1 leg's.
-cd "${GRAFT_REPO_ROOT:-/root/repo}"; R=$(pwd); OUT=$R/gpurun_out/${TAG:-r05a}; mkdir -p $OUT
+cd "${GRAFT_REPO_ROOT:-/root/repo}"; R=$(pwd); OUT=$R/gpurun_out/${TAG:-final}; mkdir -p $OUT
 bash tools/gpu_check.sh || exit 1
 CPG_BENCH_BACKEND=gloo timeout -k 10 400 python bench.py --gpus 2 --steps 5 --warmup 2 --settle-ms 0 \
     > $OUT/c3_gloo2.out 2> $OUT/c3_gloo2.err || { tail -20 $OUT/c3_gloo2.err; exit 1; }
