@@ -483,8 +483,13 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
     # the training pass on a CU-masked stream of ntc compute units (0: every CU), the decode
     # at high priority on all of them
     s_tr = D.cu_stream(local, list(range(ntc))) if ntc else torch.cuda.Stream()
-    s_halo, s_dec, s_red, s_isl = (torch.cuda.Stream(), torch.cuda.Stream(priority=-1 if args.prio else 0),
-                                   torch.cuda.Stream(), torch.cuda.Stream())
+    s_dec = torch.cuda.Stream(priority=-1 if args.prio else 0)
+    # N = 1: no halo, no collective, no gather — the training stream runs the merge itself and no
+    # other stream is made.  Streams beyond the hardware queues (GPU_MAX_HW_QUEUES, 4) share
+    # queues, and a cross-stream wait queued behind one stream's kernels then holds the other's:
+    # with five streams the C3 steps had joined at every step boundary (profiles/r05_c3q/)
+    s_halo, s_red, s_isl = ((torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream())
+                            if world > 1 else (None, s_tr, None))
     ev = {k: [torch.cuda.Event() for _ in range(2)] for k in
           ("halo", "tr_done", "dec_done", "rec", "red", "isl")}
     # several ranks on ONE GPU (the CPG_BENCH_BACKEND=gloo rehearsal on a one-GPU box): their
@@ -518,7 +523,27 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
         e0.copy_(cdist.merge_counts_f64(e0.cpu()).to(dev))
     model1 = baumwelch.normalize(e0.cpu().numpy())
 
+    def step1(k, timed):   # N = 1: two streams, no cross-stream event
+        b = k & 1
+        bp, bs = bufs[b]
+        with torch.cuda.stream(s_dec):
+            D.decode(ctx, model1, bp[de_o // 16:], de_n, DECODE, cap=icap, first_chunk=pl.d0,
+                     sign_out=so, score=score, out=iout[b], count=icnt[b])
+        with torch.cuda.stream(s_tr):
+            mark = timed and k % 4 == 0
+            if mark:
+                ea, eb = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+                ea.record(s_tr)
+            D.train_pass(ctx, model0, bp[tr_o // 16:], bs[tr_o // 32:], tr_n, TRAIN,
+                         estep_out=rec[b][1], counts_out=rec[b][2])
+            if mark:
+                eb.record(s_tr)
+                ntr.append((ea, eb))
+            cdist.merge_train_records(ctx, rec[b][0], emerged, lmerged, gathered=gath[b])
+
     def step(k, timed):
+        if world == 1:
+            return step1(k, timed)
         b = k & 1
         bp, bs = bufs[b]
         with torch.cuda.stream(s_halo):
