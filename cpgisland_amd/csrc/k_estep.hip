@@ -315,7 +315,9 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
                                             double* __restrict__ out,
                                             const uint32_t* __restrict__ sign,
                                             unsigned long long* __restrict__ cacc,
-                                            int64_t* __restrict__ cout) {
+                                            int64_t* __restrict__ cout, int64_t c, bool fresh) {
+    // c: the chunk; fresh: the model's tables are not in LDS yet (a persistent workgroup's
+    // first chunk, or every chunk of a one-chunk workgroup)
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     const int nl = blockDim.x;             // lanes = C / 64
     const int nw = nl / 64;                // waves
@@ -326,23 +328,31 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
     // buffer (phase 2), the xi bins (phase 3) — each phase ends with a barrier
     double2* T2A = TB + 16;                                   // 2-step (P(+,+), P(+,-))
     double2* T2B = T2A + kKeys;                               // 2-step (P(-,+), P(-,-))
-    double2* TA4 = reinterpret_cast<double2*>(smem + kUnionOff);   // 4-step products, row 0
     auto* part = reinterpret_cast<unsigned long long*>(
         smem + kUnionOff + kUnionBytes);
-    double2* fck = reinterpret_cast<double2*>(part + 16 * 64);   // [NMB][nl] alpha checkpoints
+    // alpha checkpoints [NMB][nl] (kRep: mini-blocks 1.. only, [NMB - 1][nl]; mini-block 0's
+    // stays in registers)
+    double2* fck = reinterpret_cast<double2*>(part + 16 * 64);
+    constexpr int kCkLds = kRep ? kLanePos / 16 - 1 : kLanePos / 16;
+    // kRep: the lane-private row copy of the 64 trinucleotide keys (the one-step keys of lane
+    // 0's first block are read from T2A / T2B), then the 4-step tables — all built once per
+    // persistent workgroup; otherwise the 4-step tables live in the union, rebuilt per chunk
+    double2* RA = fck + (size_t)kCkLds * nl;
+    double2* RB = RA + 64 * 16;
+    double2* TA4 = kRep ? RB + 64 * 16 : reinterpret_cast<double2*>(smem + kUnionOff);
     unsigned char* uni = smem + kUnionOff;   // scan buffer (phase 2), xi bins (phase 3)
-    double2* TB4 = TA4 + 1024;                                //                  row 1
+    double2* TB4 = TA4 + 1024;                                // 4-step products, rows 0 / 1
     auto* bins = reinterpret_cast<unsigned long long*>(uni);  // [64 rows][16 columns]
-    const int t = threadIdx.x;
+    // the thread index from an opaque copy made per chunk: in the persistent form the compiler
+    // would otherwise keep every lane-derived address live across the whole loop (spills)
+    int t = threadIdx.x;
+    if (kRep) asm volatile("" : "+v"(t));
     const int lane = t & 63;
-    const int64_t c = blockIdx.x;
     const uint32_t* pk = packed + c * (C / 16);
     // the one- and two-step rows from the model's cached table (est_tables: L2-resident, 3 KB)
     // rather than per-lane reads of the kernel-argument model
-    for (int i = t; i < 32 + 2 * kKeys; i += nl) TA[i] = gtab[i];   // TB, T2A, T2B follow TA
-    double2* RA = reinterpret_cast<double2*>(reinterpret_cast<unsigned char*>(fck) +
-                                             (size_t)(kLanePos / 16) * nl * sizeof(double2));
-    double2* RB = RA + kKeys * 16;
+    if (fresh)
+        for (int i = t; i < 32 + 2 * kKeys; i += nl) TA[i] = gtab[i];   // TB, T2A, T2B follow TA
     // (kRep: the lane-private row copy is made by waves 1.. while wave 0 walks the rows, 2c)
     const double2* __restrict__ rA = RA + (t & 15);   // this lane's column of the copy
     const double2* __restrict__ rB = RB + (t & 15);
@@ -375,6 +385,7 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
     // 4-step products: window (b0..b4) -> M(b0,b1) M(b1,b2) M(b2,b3) M(b3,b4), from the rows
     // (computing them here measured faster than copying a per-model table: 32 KB of L2 reads
     // per workgroup)
+    if (!kRep || fresh)
     for (int i = t; i < 1024; i += nl) {
         double x00 = 1.0, x01 = 0.0, x10 = 0.0, x11 = 1.0;
 #pragma unroll
@@ -505,8 +516,8 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
         // every lane is past its 4-step table reads (phase 1, before the barrier above): the
         // union becomes the bins
         for (int i = t - 64; i < kKeyRows * 16; i += nl - 64) bins[i] = 0ull;
-        if (kRep)
-            for (int i = t - 64; i < kKeys * 16; i += nl - 64) {
+        if (kRep && fresh)
+            for (int i = t - 64; i < 64 * 16; i += nl - 64) {
                 RA[i] = gtab[32 + (i >> 4)];
                 RB[i] = gtab[32 + kKeys + (i >> 4)];
             }
@@ -554,9 +565,10 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
         const double4 A = Pk[m - 1];
         double xP = aP * A.x + aM * A.z, xM = aP * A.y + aM * A.w;
         vnorm(xP, xM);
-        fck[m * nl + t] = make_double2(xP, xM);
+        fck[(m - (kRep ? 1 : 0)) * nl + t] = make_double2(xP, xM);
     }
-    fck[t] = make_double2(aP, aM);
+    if (!kRep) fck[t] = make_double2(aP, aM);
+    const double2 ck0 = make_double2(aP, aM);   // (kRep: mini-block 0's checkpoint, see 3b)
     // (no barrier: a lane reads only its own checkpoints; the bins were zeroed before the
     // walk's barrier)
 
@@ -583,6 +595,10 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
     const double2* __restrict__ g2a = gtab + 32;          // backward rows (global, L1-resident)
     const double2* __restrict__ g2b = gtab + 32 + kKeys;
     double yP = bP, yM = bM;   // beta at the last position of the mini-block
+    // kRep rows: the 64 trinucleotide keys from this lane's column of the copy, the one-step
+    // keys (64 ..: lane 0's first block only) from T2A / T2B — one load from a selected address
+    auto repA = [&](uint32_t kk) { return *(kk < 64u ? rA + kk * 16 : T2A + kk); };
+    auto repB = [&](uint32_t kk) { return *(kk < 64u ? rB + kk * 16 : T2B + kk); };
 #pragma unroll 1
     for (int m = NMB - 1; m >= 0; --m) {
         // the mini-block's bases from its packed word and the last base of the word before:
@@ -595,7 +611,12 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
             const uint32_t k = (uint32_t)(cm >> (4 * j)) & 63u;
             return (j == 0 && sp) ? 64u + (k >> 2) : k;
         };
-        const double2 f = fck[m * nl + t];   // alpha at the position before the mini-block
+        // alpha at the position before the mini-block.  kRep: mini-block m >= 1's from slot
+        // m - 1; the last mini-block's slot, read first, then takes mini-block 0's (its
+        // register dies here)
+        const int ci = kRep ? (m == 0 ? NMB - 2 : m - 1) : m;
+        const double2 f = fck[ci * nl + t];
+        if (kRep && m == NMB - 1) fck[(NMB - 2) * nl + t] = ck0;
         constexpr int kB = kMB / 2;          // blocks per mini-block
         double alP[kB], alM[kB];
         // alpha renormalised after every kRNB blocks (2: positions 3, 7, 11, 15, i.e. A_2, A_4,
@@ -610,16 +631,16 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
         double2 fa[kFPD + 1], fb[kFPD + 1];
 #pragma unroll
         for (int j = 0; j < kFPD; ++j) {
-            fa[j] = kRep ? rA[key(j) * 16] : T2A[key(j)];
-            fb[j] = kRep ? rB[key(j) * 16] : T2B[key(j)];
+            fa[j] = kRep ? repA(key(j)) : T2A[key(j)];
+            fb[j] = kRep ? repB(key(j)) : T2B[key(j)];
         }
 #pragma unroll
         for (int j = 0; j < kB; ++j) {
             alP[j] = xP;
             alM[j] = xM;
             if (j + kFPD < kB) {
-                fa[(j + kFPD) % (kFPD + 1)] = kRep ? rA[key(j + kFPD) * 16] : T2A[key(j + kFPD)];
-                fb[(j + kFPD) % (kFPD + 1)] = kRep ? rB[key(j + kFPD) * 16] : T2B[key(j + kFPD)];
+                fa[(j + kFPD) % (kFPD + 1)] = kRep ? repA(key(j + kFPD)) : T2A[key(j + kFPD)];
+                fb[(j + kFPD) % (kFPD + 1)] = kRep ? repB(key(j + kFPD)) : T2B[key(j + kFPD)];
             }
             __builtin_amdgcn_sched_barrier(0);
             const double2 ma = fa[j % (kFPD + 1)], mb = fb[j % (kFPD + 1)];
@@ -640,8 +661,8 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
 #pragma unroll
         for (int j = 0; j < kPFD; ++j) {
             const uint32_t k = key(kB - 1 - j);
-            qa[j] = kRep ? rA[k * 16] : g2a[k];
-            qb[j] = kRep ? rB[k * 16] : g2b[k];
+            qa[j] = kRep ? repA(k) : g2a[k];
+            qb[j] = kRep ? repB(k) : g2b[k];
         }
 #pragma unroll
         for (int j = kB - 1; j >= 0; --j) {
@@ -649,8 +670,8 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
             // sinking them to their use (one L1/L2 round trip on every block's chain)
             if (j - kPFD >= 0) {
                 const uint32_t k = key(j - kPFD);
-                qa[(kB - 1 - j + kPFD) % (kPFD + 1)] = kRep ? rA[k * 16] : g2a[k];
-                qb[(kB - 1 - j + kPFD) % (kPFD + 1)] = kRep ? rB[k * 16] : g2b[k];
+                qa[(kB - 1 - j + kPFD) % (kPFD + 1)] = kRep ? repA(k) : g2a[k];
+                qb[(kB - 1 - j + kPFD) % (kPFD + 1)] = kRep ? repB(k) : g2b[k];
             }
             __builtin_amdgcn_sched_barrier(0);
             const uint32_t k = key(j);
@@ -738,17 +759,35 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
                    unsigned int* done, double* __restrict__ out,
                    const uint32_t* __restrict__ sign, unsigned long long* __restrict__ cacc,
                    int64_t* __restrict__ cout) {
-    estep_chunk<kCnt, false>(model, packed, C, acc, gtab, done, out, sign, cacc, cout);
+    estep_chunk<kCnt, false>(model, packed, C, acc, gtab, done, out, sign, cacc, cout, blockIdx.x,
+                             true);
 }
-// the long launches' form (kRep): lane-private row copies, the registers of 4 waves per SIMD
+// the long launches' form (kRep): lane-private row copies, the registers of 4 waves per SIMD,
+// and kRepRun consecutive chunks per workgroup — the model's tables, the lane-private row copy
+// and the 4-step tables made once per workgroup instead of once per chunk, kRepRun - 1
+// workgroup launches fewer.  (Persistent workgroups, one per CU taking chunks from a work
+// counter, were faster alone but never gave a compute unit back: beside the decode stream
+// they starved its kernels for milliseconds; a run of a few chunks returns each CU every
+// ~0.1 ms.)
+#ifndef CPG_EST_REP_RUN
+#define CPG_EST_REP_RUN 4
+#endif
+constexpr int kRepRun = CPG_EST_REP_RUN;
 template <bool kCnt>
 __global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(kWavesPerEURep)))
 void k_estep_chunk_rep(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
                        unsigned long long* __restrict__ acc, const double2* __restrict__ gtab,
-                       unsigned int* done, double* __restrict__ out,
-                       const uint32_t* __restrict__ sign, unsigned long long* __restrict__ cacc,
-                       int64_t* __restrict__ cout) {
-    estep_chunk<kCnt, true>(model, packed, C, acc, gtab, done, out, sign, cacc, cout);
+                       double* __restrict__ out, const uint32_t* __restrict__ sign,
+                       unsigned long long* __restrict__ cacc, int64_t* __restrict__ cout,
+                       int64_t nchunks) {
+    // chunks blockIdx.x + i * gridDim.x: the workgroups running at one time hold consecutive
+    // chunks, so their accumulator replicas (c % kAccRep) are all in use (runs of consecutive
+    // chunks per workgroup put every resident workgroup on a quarter of them)
+    for (int64_t c = blockIdx.x, i = 0; i < kRepRun && c < nchunks; ++i, c += gridDim.x) {
+        estep_chunk<kCnt, true>(model, packed, C, acc, gtab, nullptr, out, sign, cacc, cout, c,
+                                i == 0);
+        __syncthreads();   // (the chunk's LDS reads are done before the next chunk's writes)
+    }
 }
 
 
@@ -867,9 +906,10 @@ size_t estep_ws_bytes(int64_t, int64_t) { return (size_t)2 * kSlab * 8 * kAccRep
 
 namespace {
 size_t estep_lds(int lanes, bool rep) {   // the union is sized for 16 waves; fewer lanes use a prefix
-    const size_t ck = (size_t)(kLanePos / 16) * lanes * sizeof(double2);
+    // (kRep: checkpoints of mini-blocks 1.., the 64-key row copy, the 4-step tables)
+    const size_t ck = (size_t)(kLanePos / 16 - (rep ? 1 : 0)) * lanes * sizeof(double2);
     return kUnionOff + kUnionBytes + 16 * 64 * sizeof(unsigned long long) + ck +
-           (rep ? (size_t)kKeys * 16 * 2 * sizeof(double2) : 0);
+           (rep ? ((size_t)64 * 16 * 2 + 2 * 1024) * sizeof(double2) : 0);
 }
 // The lane-private row copy (kRep) makes the pass itself 7-10 % faster (46 Mbp: 0.0959 ->
 // 0.0887 ms; 3.1 Gbp: 4.89 -> 4.38 ms) but takes 40 KB of LDS from the decode kernels that
@@ -886,6 +926,7 @@ constexpr int64_t kEstRepMinChunks = CPG_EST_REP_MIN;
 #define CPG_EST_SEPFIN_MIN 2048
 #endif
 constexpr int64_t kEstSepFinMinChunks = CPG_EST_SEPFIN_MIN;
+unsigned est_rep_grid(int64_t nchunks) { return (unsigned)((nchunks + kRepRun - 1) / kRepRun); }
 }  // namespace
 
 hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t nchunks,
@@ -900,10 +941,10 @@ hipError_t launch_estep(const cpg_model& model, const uint32_t* packed, int64_t 
         const bool sepfin = parts == PART_ALL && nchunks >= kEstSepFinMinChunks;
         unsigned int* done = parts == PART_ALL && !sepfin
                                  ? reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep) : nullptr;
-        if (nchunks >= kEstRepMinChunks)
-            hipLaunchKernelGGL((k_estep_chunk_rep<false>), dim3((unsigned)nchunks), dim3(lanes),
-                               estep_lds(lanes, true), s, model, packed, C, acc, gtab, done, out,
-                               nullptr, nullptr, nullptr);
+        if (nchunks >= kEstRepMinChunks && !done)
+            hipLaunchKernelGGL((k_estep_chunk_rep<false>), dim3(est_rep_grid(nchunks)),
+                               dim3(lanes), estep_lds(lanes, true), s, model, packed, C, acc, gtab,
+                               out, nullptr, nullptr, nullptr, nchunks);
         else
             hipLaunchKernelGGL((k_estep_chunk<false>), dim3((unsigned)nchunks), dim3(lanes),
                                estep_lds(lanes, false), s, model, packed, C, acc, gtab, done, out,
@@ -935,10 +976,10 @@ hipError_t launch_train(const cpg_model& model, const uint32_t* packed, const ui
     const bool sepfin = nchunks >= kEstSepFinMinChunks;
     unsigned int* done =
         sepfin ? nullptr : reinterpret_cast<unsigned int*>(acc + 2 * kSlab * kAccRep);
-    if (nchunks >= kEstRepMinChunks)
-        hipLaunchKernelGGL((k_estep_chunk_rep<true>), dim3((unsigned)nchunks), dim3(lanes),
-                           estep_lds(lanes, true), s, model, packed, C, acc, gtab, done, out, sign,
-                           cacc, cout);
+    if (nchunks >= kEstRepMinChunks && !done)
+        hipLaunchKernelGGL((k_estep_chunk_rep<true>), dim3(est_rep_grid(nchunks)), dim3(lanes),
+                           estep_lds(lanes, true), s, model, packed, C, acc, gtab, out, sign, cacc,
+                           cout, nchunks);
     else
         hipLaunchKernelGGL((k_estep_chunk<true>), dim3((unsigned)nchunks), dim3(lanes),
                            estep_lds(lanes, false), s, model, packed, C, acc, gtab, done, out, sign,

@@ -24,7 +24,7 @@ extern "C" int cpg_dbg_stamps(unsigned long long* h, int n) {
 # (anchor, stamp index, before|after): the phase boundaries of k_estep_chunk
 ANCHORS = [
     ("    const uint32_t* pk = packed + c * (C / 16);\n", 0, "after"),
-    ("    if (kCnt) {   // the lane's 64 bases", 1, "before"),
+    ("    // the lane's 64 bases = one count block", 1, "before"),
     ("    // 4-step products: window (b0..b4)", 2, "before"),
     ("    constexpr int L = kLanePos;            // 64 positions per lane", 3, "before"),
     ("    // 2. ", 4, "before"),
