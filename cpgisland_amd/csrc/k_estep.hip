@@ -535,8 +535,14 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
     __syncthreads();
     // the union has become the bins: zeroed by waves 1.. during the walk (2c), or here by the
     // only wave (its own LDS accesses stay in order: no barrier before the main loop either)
-    if (nl == 64)
+    if (nl == 64) {
         for (int i = t; i < kKeyRows * 16; i += nl) bins[i] = 0ull;
+        if (kRep && fresh)   // (the one wave makes the row copy too: chunks of 4,096 bases)
+            for (int i = t; i < 64 * 16; i += nl) {
+                RA[i] = gtab[32 + (i >> 4)];
+                RB[i] = gtab[32 + kKeys + (i >> 4)];
+            }
+    }
     unsigned long long* racc = acc + 2 * kSlab * (c % kAccRep);
     if (t == nl - 1) {   // the chunk log-likelihood, in signed 2^-24 units (added now: nothing
                          // stays live across the main loop)
