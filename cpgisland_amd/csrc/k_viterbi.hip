@@ -294,6 +294,18 @@ __device__ __forceinline__ const VitDerived* derived(const VitTables* vt) {
 // lookup ring below (profiles/r02_v10/ab_k5_occupancy*.log).  K3 at 8 (spills) and K7 at 8 (75
 // spills) were slower; K1 cannot reach 64 at its LDS (the slim-LDS variant at 64 lost 1.5 %).
 constexpr int kK5WavesPerEU = 8;
+// the fused form (K6 inside: decodes of <= 256 chunks, tail_fusion_pays) runs ~3 waves per
+// SIMD — too few to cover a step's table-lookup latency with one another — so its lookups are
+// issued kK5LookFused steps ahead (the registers for them: 2 ahead fits the 64 of 8 waves per
+// SIMD that the long decodes' form keeps)
+#ifndef CPG_K5_LOOK_FUSED
+#define CPG_K5_LOOK_FUSED 4
+#endif
+#ifndef CPG_K5_WPE_FUSED
+#define CPG_K5_WPE_FUSED 6
+#endif
+constexpr int kK5LookFused = CPG_K5_LOOK_FUSED;
+constexpr int kK5WavesPerEUFused = CPG_K5_WPE_FUSED;
 __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables* vt) {
     VitDerived* dv = reinterpret_cast<VitDerived*>(vt + 1);
     const int n = kQ4 + kMaxBinade * 16 + kMaxBinade * 64 + kMaxBinade * kW4;
@@ -1737,6 +1749,7 @@ __device__ __forceinline__ uint32_t quad_origin(uint64_t hP, uint64_t hM) {
 // one block's re-forward (lane = block gid): backpointers, the self-check; returns the
 // block's origin map
 // sgi: the segment (workgroup of the segment path) the block belongs to.
+template <int kLook>
 __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_t* packed,
                                               const Geo& g, const uint8_t* __restrict__ degen,
                                               const double2* __restrict__ entry,
@@ -1817,8 +1830,7 @@ __device__ __forceinline__ uint32_t fwd_block(const VitConsts& vc, const uint32_
     };
     if (g.whole(k)) {
         // quads of 64 steps; the ring of kLook lookups in flight runs across quad borders
-        // (2 deep: at the 64-VGPR budget, 4 had spilled more and measured slower)
-        constexpr int kLook = 2;
+        static_assert(64 % kLook == 0, "the ring's slot of a step is its index mod kLook in every quad");
         const unsigned char* LAb = reinterpret_cast<const unsigned char*>(LA);
         const unsigned char* LBb = reinterpret_cast<const unsigned char*>(LB);
         auto fetch = [&](uint32_t a) {   // a = code * 16 (byte offset of the entry)
@@ -1998,7 +2010,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_tscan(Geo g, const double2* __
 // that workgroup); the origin maps then cross workgroups inside the kernel, 4 per
 // agent-scope atomic word.
 template <bool kScan>
-__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kK5WavesPerEU))) void k_vit_forward(VitConsts vc, const uint32_t* packed,
+__global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kScan ? kK5WavesPerEUFused : kK5WavesPerEU))) void k_vit_forward(VitConsts vc, const uint32_t* packed,
                                                           Geo g, const uint8_t* __restrict__ degen,
                                                           const double2* __restrict__ entry,
                                                           uint4* __restrict__ bp,
@@ -2024,7 +2036,7 @@ __global__ __launch_bounds__(kThreads) __attribute__((amdgpu_waves_per_eu(kK5Wav
     __syncthreads();
     const int64_t gid = (int64_t)blockIdx.x * kThreads + threadIdx.x;
     if (gid >= g.nchunks * g.nsb) return;   // (kScan: the grid is whole workgroups)
-    const uint32_t org = fwd_block(vc, packed, g, degen, entry, bp, status, rx, seg, went, LA,
+    const uint32_t org = fwd_block<kScan ? kK5LookFused : 2>(vc, packed, g, degen, entry, bp, status, rx, seg, went, LA,
                                    LB, gid, blockIdx.x);
     if constexpr (!kScan) {
         origin[gid] = (uint8_t)org;
