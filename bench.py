@@ -186,30 +186,55 @@ def decode_step(ctx, model1, dp, N, so, score, iout, icnt, fused, first_chunk=0)
                   count=icnt)
 
 
-def cold_cache_steps(ln, dp, ds, N, model0, model1, nsteps, main_s, dev, flush_mb=1024,
+def cold_cache_steps(ln, dp, ds, N, model0, model1, nsteps, main_s, dev, first_chunk, flush_mb=1024,
                      fused=True, fused_decode=True):
-    """The step on one stream, each behind a 1 GiB scratch write that evicts the shard from
-    the 256 MB Infinity Cache; HIP events bracket the step's kernels only (not the flush)."""
-    from cpgisland_amd import device as D
+    """The headline step's two streams (training pass on the lane's training stream, decode on
+    its high-priority decode stream, concurrently), each step behind a `flush_mb` scratch write
+    that evicts the shard from the 256 MB Infinity Cache (SURVEY 8(d)'s protocol).  Events: one
+    on the main stream after the flush (both streams wait on it), one at the end of each
+    stream's work; a step's time = the later end - that start, so the flush is excluded.  The
+    same joined steps without the flush are timed beside it (`warm_joined_ms`): the cold/warm
+    ratio is the Infinity Cache's share at equal step structure (the headline itself also
+    overlaps consecutive steps, which a flush between steps rules out)."""
     buf = torch.empty(flush_mb << 18, dtype=torch.float32, device=dev)
-    pairs = []
-    with torch.cuda.stream(main_s):
+    s_tr, s_dec = ln["s_tr"], ln["s_dec"]
+    ctx = ln["ctx"]
+
+    def joined(flush):
+        marks = []
         for _ in range(nsteps):
-            buf.fill_(1.0)
-            a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-            a.record()
-            train_step(ln["ctx"], model0, dp, ds, N, ln["ecnt"], ln["lcnt"], fused)
-            decode_step(ln["ctx"], model1, dp, N, ln["so"], ln["score"], ln["iout"], ln["icnt"],
-                        fused_decode)
-            b.record()
-            pairs.append((a, b))
-    torch.cuda.synchronize()
-    ln["ctx"].sync(None)
-    ms = sum(a.elapsed_time(b) for a, b in pairs) / len(pairs)
+            with torch.cuda.stream(main_s):
+                if flush:
+                    buf.fill_(1.0)
+                e0 = torch.cuda.Event(enable_timing=True)
+                e0.record(main_s)
+            s_dec.wait_event(e0)
+            s_tr.wait_event(e0)
+            with torch.cuda.stream(s_dec):
+                decode_step(ctx, model1, dp, N, ln["so"], ln["score"], ln["iout"], ln["icnt"],
+                            fused_decode, first_chunk)
+                ed = torch.cuda.Event(enable_timing=True)
+                ed.record(s_dec)
+            with torch.cuda.stream(s_tr):
+                train_step(ctx, model0, dp, ds, N, ln["ecnt"], ln["lcnt"], fused)
+                et = torch.cuda.Event(enable_timing=True)
+                et.record(s_tr)
+            main_s.wait_event(ed)
+            main_s.wait_event(et)
+            marks.append((e0, ed, et))
+        torch.cuda.synchronize()
+        ctx.sync(None)
+        return sum(max(a.elapsed_time(b), a.elapsed_time(c)) for a, b, c in marks) / len(marks)
+    joined(False)   # (first use of this step shape: untimed)
+    warm = joined(False)
+    cold = joined(True)
     del buf
-    return {"value": N / (ms / 1e3), "unit": "bases/s", "ms_per_step": round(ms, 4),
-            "steps": nsteps, "flush_mb": flush_mb, "streams": 1,
-            "note": "one stream, no step overlap (compare the --serial warm rate)"}
+    return {"value": N / (cold / 1e3), "unit": "bases/s", "ms_per_step": round(cold, 4),
+            "warm_joined_ms": round(warm, 4), "cold_over_warm": round(cold / warm, 4),
+            "steps": nsteps, "flush_mb": flush_mb, "streams": 2, "step_overlap": False,
+            "note": ("the headline's two concurrent streams per step, each step behind a 1 GiB "
+                     "scratch write (excluded by events); warm_joined_ms: the same joined steps "
+                     "without the flush")}
 
 
 def _cpu_model():
@@ -290,6 +315,62 @@ def sha256_hex(*arrays):
     for a in arrays:
         h.update(np.ascontiguousarray(a).view(np.uint8).tobytes())
     return h.hexdigest()
+
+
+def oracle_fixture(name, seed, start, nbases):
+    """The oracle's whole-genome results for this workload (tests/golden/fingerprints.json,
+    cpgisland_amd/fingerprint.py), or None when the workload is not the digested one."""
+    from cpgisland_amd import fingerprint as F
+    try:
+        fx = F.load().get(name)
+    except (OSError, ValueError):
+        return None
+    if not fx or (fx["seed"], fx["start"], fx["nbases"]) != (seed, start, nbases):
+        return None
+    return fx
+
+
+def decode_model(fx, fallback):
+    """The decode model: the fixture's committed one-iteration model (bit patterns: the GPU
+    and the oracle decode with identical constants), else fallback() (a GPU E-step + the
+    reducer, for workloads the fixture does not cover)."""
+    from cpgisland_amd import HmmModel
+    from cpgisland_amd import fingerprint as F
+    if fx is not None:
+        return HmmModel.from_struct(F.hex_to_f64(fx["decode"]["model_hex"]))
+    return fallback()
+
+
+def c2_fingerprint(fx, so, score, iout, icnt, ecnt, lcnt, ndec, nsplit):
+    """Digest of one C2 step's results and, for the digested genome, the comparison with the
+    oracle's results over every chunk (cpgisland_amd/fingerprint.py)."""
+    from cpgisland_amd import device as D
+    from cpgisland_amd import fingerprint as F
+    if nsplit != 1:
+        return {"oracle_match": None, "note": "--decode-split: records spread over parts"}
+    dd = F.decode_digest(so.cpu().numpy(), score.cpu().numpy(), D.islands_to_numpy(iout, icnt),
+                         ndec, DECODE, per_chunk=fx is not None)
+    est, cnt = ecnt.cpu().numpy()[:105], lcnt.cpu().numpy()
+    fp = {"path_sha256": dd["path_sha256"], "records_sha256": dd["records_sha256"],
+          "counts_sha256": sha256_hex(cnt), "islands": dd["islands"], "oracle_match": None}
+    if fx is not None:
+        r = F.compare(fx, estep=est, counts=cnt, decode=dd)
+        fp.update({k: r[k] for k in ("counts", "estep", "estep_max_rel_err", "path", "scores",
+                                     "records", "oracle_match")})
+        fp["oracle"] = ("tests/golden/fingerprints.json C2: oracle/cpg_oracle.c over all "
+                        f"{fx['train']['chunks']} training and {fx['decode']['chunks']} decode "
+                        "chunks; the decode model is its committed one-iteration model")
+    return fp
+
+
+def chunks_match(fx, sign_words, scores, c0, c1):
+    """This rank's decode chunks [c0, c1) against the fixture's per-chunk path digests and
+    scores: (path_ok, scores_ok)."""
+    from cpgisland_amd import fingerprint as F
+    fd = fx["decode"]
+    dig = F.chunk_digests(sign_words, c1 - c0, DECODE)
+    sc = F.f64_to_hex(np.asarray(scores, np.float64)[: c1 - c0])
+    return dig == fd["chunk_path_digests"][c0:c1], sc == fd["scores_hex"][c0:c1]
 
 
 def bw_iteration_leg(ctx, estep_fn, decode_fn, nbases, iters, dist, dev, backend="nccl"):
@@ -516,12 +597,16 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
     for b in range(2):
         halo_into(b)
     torch.cuda.synchronize()
-    e0 = D.bw_estep(ctx, model0, bufs[0][0][tr_o // 16:], tr_n, TRAIN)
-    if dist and backend == "nccl":
-        cdist.merge_counts_f64(e0)
-    elif dist:
-        e0.copy_(cdist.merge_counts_f64(e0.cpu()).to(dev))
-    model1 = baumwelch.normalize(e0.cpu().numpy())
+    fx = oracle_fixture("C3", C3_SEED, 0, G)
+
+    def gpu_model1():
+        e0 = D.bw_estep(ctx, model0, bufs[0][0][tr_o // 16:], tr_n, TRAIN)
+        if dist and backend == "nccl":
+            cdist.merge_counts_f64(e0)
+        elif dist:
+            e0.copy_(cdist.merge_counts_f64(e0.cpu()).to(dev))
+        return baumwelch.normalize(e0.cpu().numpy())
+    model1 = decode_model(fx, gpu_model1)
 
     def step1(k, timed):   # N = 1: two streams, no cross-stream event
         b = k & 1
@@ -613,14 +698,47 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
     # construction): the island records gathered on rank 0 in chunk order (rank order = chunk
     # order, each rank's in chunk order) and the merged labelled int64 counts
     fp = None
+    # against the oracle (every chunk: tests/golden/fingerprints.json): each rank checks its own
+    # decode chunks' paths and scores, one MIN all-reduce; rank 0 the gathered records and the
+    # merged counts / E-step
+    chk = None
+    if fx is not None:
+        pth, scs = chunks_match(fx, so.cpu().numpy().view(np.uint32), score.cpu().numpy(),
+                                pl.d0, pl.d1)
+        chk = torch.tensor([int(pth), int(scs)], dtype=torch.int64, device=dev)
+        if dist:
+            if backend == "nccl":
+                torch.distributed.all_reduce(chk, op=torch.distributed.ReduceOp.MIN)
+            else:
+                h = chk.cpu()
+                torch.distributed.all_reduce(h, op=torch.distributed.ReduceOp.MIN)
+                chk = h
+        chk = [bool(x) for x in chk.tolist()]
     if rank == 0:
         if world > 1:
             recs = np.concatenate([gat_i[last][r][:counts[r]].cpu().numpy().reshape(-1)
                                    for r in range(world)])
         else:
             recs = iout[last][:counts[0]].cpu().numpy().reshape(-1)
-        fp = {"records_sha256": sha256_hex(recs), "counts_sha256": sha256_hex(lmerged.cpu().numpy()),
-              "islands": int(sum(counts))}
+        lm = lmerged.cpu().numpy()
+        fp = {"records_sha256": sha256_hex(recs), "counts_sha256": sha256_hex(lm),
+              "islands": int(sum(counts)), "oracle_match": None}
+        if fx is not None:
+            from cpgisland_amd import fingerprint as F
+            ok, rel = F.estep_close(emerged.cpu().numpy()[:105], fx["train"]["estep_hex"],
+                                    fx["train"]["estep_bound_hex"])
+            parts = {"counts": bool(np.array_equal(lm, np.asarray(fx["train"]["counts"], np.int64))),
+                     "estep": ok,
+                     "path": chk[0], "scores": chk[1],
+                     "records": (sha256_hex(recs) == fx["decode"]["records_sha256"] and
+                                 int(sum(counts)) == fx["decode"]["islands"])}
+            fp.update(parts)
+            fp["estep_max_rel_err"] = rel
+            fp["oracle_match"] = all(parts.values())
+            fp["oracle"] = ("tests/golden/fingerprints.json C3: oracle/cpg_oracle.c over all "
+                            f"{fx['train']['chunks']} training and {fx['decode']['chunks']} "
+                            "decode chunks; the decode model is its committed one-iteration "
+                            "model")
     bw = None
     if args.bw_iters > 0:
         def dec_fn(m):
@@ -773,10 +891,11 @@ def main():
                          "overlap)")
     ap.add_argument("--flush-mb", type=int, default=0,
                     help="write this many MiB of scratch between steps (cold Infinity Cache)")
-    ap.add_argument("--cold-steps", type=int, default=5,
-                    help="N=1: after the timed region, this many extra one-stream steps each "
+    ap.add_argument("--cold-steps", type=int, default=10,
+                    help="N=1: after the timed region, this many extra two-stream steps each "
                          "behind a 1 GiB scratch write (cold Infinity Cache), reported as "
-                         "cold_cache beside the headline (0 = skip)")
+                         "cold_cache beside the headline with the same joined steps warm "
+                         "(0 = skip)")
     args = ap.parse_args()
     if args.flush_mb:
         args.serial = True   # the flushed step time is the sum of isolated phase times
@@ -854,13 +973,19 @@ def main():
         cx.reserve(N)
         lanes.append(make_lane(cx))
 
-    # trained model for the decode: one Baum-Welch iteration from the reference's model
-    ecnt = lanes[0]["ecnt"]
-    D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
-    if dist:
-        cdist.merge_counts_f64(ecnt)
-    from cpgisland_amd import baumwelch
-    model1 = baumwelch.normalize(ecnt.cpu().numpy())
+    # the decode model: one Baum-Welch iteration from the reference's model — the oracle's,
+    # committed with its whole-genome results (tests/golden/fingerprints.json C2), for every
+    # rank; for other workload sizes a GPU E-step over the shard + the reducer
+    fx = oracle_fixture("C2", SEED, start, N)
+
+    def gpu_model1():
+        from cpgisland_amd import baumwelch
+        ecnt = lanes[0]["ecnt"]
+        D.bw_estep(ctx, model0, dp, N, TRAIN, out=ecnt)
+        if dist:
+            cdist.merge_counts_f64(ecnt)
+        return baumwelch.normalize(ecnt.cpu().numpy())
+    model1 = decode_model(oracle_fixture("C2", SEED, 0, N), gpu_model1)
 
     # HIP events inside the timed steps: the E-step phase (the roofline's dominant kernel) and
     # the decode phase (on every --decode-event-every-th step) by default; every phase with
@@ -1100,6 +1225,16 @@ def main():
             cx3.sync(None)
         for dl in ln["dec"][1:]:
             dl[0].sync(None)
+    # the last timed step's results (its lane's buffers) against the oracle's over the whole
+    # shard (rank 0's shard is the digested C2 genome); before the BW leg reuses the buffers
+    fingerprint = None
+    if rank == 0:
+        kl = nwarm + args.steps - 1
+        ln = lanes[kl % nlanes]
+        _, _, d_so, d_score, d_iout, d_icnt = ln["dec"][kl % ndl]
+        _, ecnt_l, lcnt_l = ln["recs"][kl % len(ln["recs"])]
+        fingerprint = c2_fingerprint(fx, d_so, d_score, d_iout, d_icnt, ecnt_l, lcnt_l, ndec,
+                                     nsplit)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         torch.distributed.all_reduce(t, op=torch.distributed.ReduceOp.MAX)
@@ -1116,7 +1251,7 @@ def main():
     cold = None
     if args.cold_steps > 0 and not dist and not args.flush_mb:
         cold = cold_cache_steps(lanes[0], dp, ds, N, model0, model1, args.cold_steps, main_s, dev,
-                                fused=fused, fused_decode=fused_decode)
+                                first_chunk, fused=fused, fused_decode=fused_decode)
     # N = 1: the C3 strong-scaling workload (the one the N > 1 lines run) on this one GPU, a
     # short leg after the headline, plus the count kernel over its HBM-resident genome
     c3_leg = None
@@ -1218,7 +1353,7 @@ def main():
                "host_issue_ms_per_step": round(issue * 1e3 / steps, 4),
                "roofline": roof, "roofline_fp64": roof_fp64, "roofline_decode": roof_decode,
                "roofline_decode_valu": roof_decode_valu, "cold_cache": cold,
-               "bw_iteration": bw}
+               "fingerprint": fingerprint, "bw_iteration": bw}
         if not args.no_cpu_baseline and world == 1:
             out["cpu_baseline"] = cpu_baseline(SEED, args.cpu_sample,
                                                 min(args.cpu_threads, os.cpu_count() or 1))

@@ -103,9 +103,6 @@ struct Lane {
                                     PHI, LO & PHI, HI & PHI, lh & PHI, pq, LO & pq, HI & pq, lh & pq};
 #pragma unroll
             for (int j = 1; j < 16; ++j) c[j] += __popc(x[j]);
-#ifdef CPG_CNT_SCHED
-            __builtin_amdgcn_sched_barrier(0);   // one pair's masks live at a time (registers)
-#endif
         }
         c[0] += valid ? (cstart ? 63u : 64u) : 0u;
         // the '+' work (rare: island blocks)

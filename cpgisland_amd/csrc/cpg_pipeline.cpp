@@ -105,7 +105,6 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
     CPG_HIP(hipSetDevice(ctx->device));
     int rc;
     if ((rc = ensure_streams(ctx))) return rc;
-    static const bool dbg_sync = std::getenv("CPG_PIPE_SYNC") != nullptr;   // diagnostic
     hipStream_t sin = ctx->ps[0], str = ctx->ps[1], sdec = ctx->ps[2], sout = ctx->ps[3];
 
     // Viterbi constants/tables of the decode model (host), before any device work
@@ -180,7 +179,6 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
             CPG_HIP(hipMemcpyAsync(buf_sign(b), sign + start / 32, (size_t)((nb + 31) / 32) * 4,
                                    hipMemcpyHostToDevice, sin));
         CPG_HIP(hipEventRecord(ev_in[b], sin));
-        if (dbg_sync) CPG_HIP(hipStreamSynchronize(sin));   // diagnostic: copy faults here
         // train: accumulate only
         CPG_HIP(hipStreamWaitEvent(str, ev_in[b], 0));
         if (estep_out && ntr > 0)
@@ -191,7 +189,6 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
             CPG_HIP(launch_count(buf_packed(b), buf_sign(b), ntr, T, static_cast<uint64_t*>(ws_cnt),
                                  nullptr, str, PART_ACC));
         CPG_HIP(hipEventRecord(ev_tr[b], str));
-        if (dbg_sync) CPG_HIP(hipStreamSynchronize(str));   // diagnostic: train kernels here
         // decode
         CPG_HIP(hipStreamWaitEvent(sdec, ev_in[b], 0));
         if (decode) {

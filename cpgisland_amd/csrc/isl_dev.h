@@ -105,6 +105,9 @@ __device__ __forceinline__ void emit_word(const WordMasks& q, int64_t w, Cnt5& e
     e.cg += __popc(q.CG);
 }
 
+constexpr int64_t kInlineBaseMax = 4096;   // chunks: write_runs sums cres inline up to here
+constexpr int kBaseBlock = 1024;            // chunks per k_isl_base workgroup
+
 struct IslWs {
     RunRec* starts;     // per tile, cap_t records
     RunRec* closes;
@@ -115,6 +118,13 @@ struct IslWs {
     // the two-pass resolve (separate island kernels: no look-back): per chunk {kept islands,
     // closed runs}; per run its kept[] word (stale_in, or -1: filtered out)
     int2* cres;
+    // past kInlineBaseMax chunks (the split path): every chunk's first record, scanned once
+    // from cres between the two passes (k_isl_base: per block of 1,024 chunks -> cbase and the
+    // block totals bsum; k_isl_bscan: the block totals' exclusive scan in place), so that
+    // write_runs reads its base instead of summing every chunk before it (O(chunks^2) work)
+    long long* cbase;
+    long long* bsum;
+    int scanned;        // 1: write_runs reads cbase[c] + bsum[c / kBaseBlock]
     int64_t ntile;      // tiles per chunk
     int64_t cap_t;      // records per tile and kind
     size_t bytes;
@@ -358,9 +368,9 @@ __device__ __forceinline__ long long kept_before(const IslWs& ws, int64_t c, uin
 // filtered (:280-285), kept islands ranked, the chunk's first record found by the look-back,
 // records written.  With <= 8 runs per lane the map and both filter outcomes (stale 0 / 1)
 // of each run stay in registers: one pass of loads before the records.
-// kSplit (the separate kernels' first pass, no look-back): the chunk's kept count and run
-// count go to ws.cres, each lane's cached bits, stale_in and rank to ws.lanest, and
-// write_runs (second pass) places the records once every chunk's count is known.
+// kSplit (the separate kernels' first pass, no look-back): every run's kept[] word (stale_in,
+// or -1: filtered out) and the chunk's {kept islands, closed runs} in ws.cres; write_runs (the
+// second pass) re-ranks from those and places the records once every chunk's count is known.
 template <bool kAgent, bool kAgentRec, bool kSplit = false>
 __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws, const Cnt5* to,
                                              int64_t c, int64_t C, int64_t nr, int32_t* kept,
@@ -530,21 +540,26 @@ __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C,
 }
 
 // The second pass of the two-pass resolve: chunk c's first record = the kept islands of the
-// chunks before it (a workgroup sum over ws.cres, written by the first pass — an earlier
-// kernel, so no workgroup waits for another), then every lane ranks and writes its kept
-// islands from the runs' kept[] words (run stats re-read for the kept runs only).
+// chunks before it (written by earlier kernels, so no workgroup waits for another: up to
+// kInlineBaseMax chunks a workgroup sum over ws.cres, past it the scanned ws.cbase + ws.bsum),
+// then every lane ranks and writes its kept islands from the runs' kept[] words (run stats
+// re-read for the kept runs only).
 __device__ __forceinline__ void write_runs(const uint32_t* packed, int64_t C, const IslWs& ws,
                                            const IslOut& o, int64_t c, long long* s_part,
                                            int32_t* sk) {
     const int t = threadIdx.x, nl = blockDim.x, lane = t & 63, wv = t >> 6;
-    long long before = 0;
-    for (int64_t j = t; j < c; j += nl) before += ws.cres[j].x;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) before += __shfl_xor(before, off);
-    if (lane == 0) s_part[wv] = before;
-    __syncthreads();
     long long base = 0;
-    for (int w = 0; w < (nl >> 6); ++w) base += s_part[w];
+    if (ws.scanned) {
+        base = ws.cbase[c] + ws.bsum[c / kBaseBlock];
+    } else {
+        long long before = 0;
+        for (int64_t j = t; j < c; j += nl) before += ws.cres[j].x;
+#pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) before += __shfl_xor(before, off);
+        if (lane == 0) s_part[wv] = before;
+        __syncthreads();
+        for (int w = 0; w < (nl >> 6); ++w) base += s_part[w];
+    }
     base += o.base_in ? *o.base_in : 0;
     const int2 cr = ws.cres[c];
     if (c == o.nchunks - 1 && t == 0) *o.count = base + cr.x;

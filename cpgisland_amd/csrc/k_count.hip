@@ -27,14 +27,9 @@ constexpr int kCntRep = cnt::kRep;
 // blocks per lane per batch, and the grid cap: 4 waves per SIMD (<= 128 VGPRs) hold 1,024
 // workgroups of 4 waves at once; every lane has two batches in flight (the one being counted
 // and the next one's loads)
-#ifndef CPG_CNT_BATCH
-#define CPG_CNT_BATCH 1
-#endif
-#ifndef CPG_CNT_GRID
-#define CPG_CNT_GRID 2048
-#endif
-constexpr int kBatch = CPG_CNT_BATCH;
-constexpr int kCntGrid = CPG_CNT_GRID;
+constexpr int kBatch = 1;
+constexpr int kCntGrid = 2048;
+constexpr int kCntWavesPerEU = 4;
 
 // the value of `v` in the lane below (wave_shr:1 DPP); lane 0 takes `old`
 __device__ __forceinline__ uint32_t from_lane_below(uint32_t v, uint32_t old) {
@@ -80,10 +75,7 @@ __device__ __forceinline__ void load_batch(Batch& b, const uint4* __restrict__ p
 // done != nullptr: the last workgroup to finish also finalizes (one launch per call).
 // kPow2: chunk_len / 64 is a power of two (the reference's 0x10000: chunk starts by a mask).
 template <bool kPow2>
-#ifndef CPG_CNT_WPE
-#define CPG_CNT_WPE 4
-#endif
-__global__ __launch_bounds__(kCountThreads) __attribute__((amdgpu_waves_per_eu(CPG_CNT_WPE)))
+__global__ __launch_bounds__(kCountThreads) __attribute__((amdgpu_waves_per_eu(kCntWavesPerEU)))
 void k_count_main(const uint4* __restrict__ packed4, const uint2* __restrict__ sign2,
                   const uint32_t* __restrict__ packed, const uint32_t* __restrict__ sign,
                   int64_t nblk, int64_t blk_per_chunk, unsigned long long* __restrict__ gacc,

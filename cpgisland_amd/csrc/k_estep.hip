@@ -285,22 +285,12 @@ __device__ void final_estep(const double* v, int t, double* __restrict__ out);
 constexpr int kWavesPerEU = 5;
 // kRep (147.5 KB of LDS: one workgroup per CU, nothing co-resides): 4 waves per SIMD, so the
 // whole 128-VGPR share of a wave is this kernel's
-#ifndef CPG_EST_WPE_REP
-#define CPG_EST_WPE_REP 4
-#endif
-constexpr int kWavesPerEURep = CPG_EST_WPE_REP;
+constexpr int kWavesPerEURep = 4;
 // table rows issued this many two-position blocks ahead of their use (forward / backward)
-#ifndef CPG_EST_FPD_REP
-#define CPG_EST_FPD_REP 1
-#endif
-#ifndef CPG_EST_PFD_REP
-#define CPG_EST_PFD_REP 1
-#endif
+constexpr int kFwdAheadRep = 1, kBwdAheadRep = 1;
 // blocks (two positions each) between the alpha renormalisations of the main loop (2: every
-// 4 positions; a build-time override for measurement builds)
-#ifndef CPG_EST_RNB
-#define CPG_EST_RNB 2
-#endif
+// 4 positions)
+constexpr int kRenormBlocks = 2;
 // kCnt: the fused training pass — each lane also counts its 64 bases' labelled transitions
 // (count_dev.h; sign = the label bits), added into the count accumulators cacc, and the last
 // workgroup finalizes both (cout: cpg_counts_i64).  Needs >= 256 lanes (chunks >= 16 Ki).
@@ -627,13 +617,13 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
         double alP[kB], alM[kB];
         // alpha renormalised after every kRNB blocks (2: positions 3, 7, 11, 15, i.e. A_2, A_4,
         // A_6, A_8); kf = the power-of-two shifts applied there
-        constexpr int kRNB = CPG_EST_RNB;
+        constexpr int kRNB = kRenormBlocks;
         int kf[kB / kRNB];
         double xP = f.x, xM = f.y;
         // the rows are issued kFPD steps ahead (the scheduling barrier keeps them there: the
         // compiler had waited for each step's reads right before using them, one LDS round
         // trip on every step of the chain)
-        constexpr int kFPD = kRep ? CPG_EST_FPD_REP : 1;   // (2: one spill at 96 VGPRs and no faster)
+        constexpr int kFPD = kRep ? kFwdAheadRep : 1;   // (2: one spill at 96 VGPRs and no faster)
         double2 fa[kFPD + 1], fb[kFPD + 1];
 #pragma unroll
         for (int j = 0; j < kFPD; ++j) {
@@ -662,7 +652,7 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
             yP *= r;
             yM *= r;
         }
-        constexpr int kPFD = kRep ? CPG_EST_PFD_REP : 1;   // backward rows this many blocks ahead
+        constexpr int kPFD = kRep ? kBwdAheadRep : 1;   // backward rows this many blocks ahead
         double2 qa[kPFD + 1], qb[kPFD + 1];
 #pragma unroll
         for (int j = 0; j < kPFD; ++j) {
@@ -775,10 +765,7 @@ void k_estep_chunk(const cpg_model model, const uint32_t* __restrict__ packed, i
 // counter, were faster alone but never gave a compute unit back: beside the decode stream
 // they starved its kernels for milliseconds; a run of a few chunks returns each CU every
 // ~0.1 ms.)
-#ifndef CPG_EST_REP_RUN
-#define CPG_EST_REP_RUN 4
-#endif
-constexpr int kRepRun = CPG_EST_REP_RUN;
+constexpr int kRepRun = 4;
 template <bool kCnt>
 __global__ __launch_bounds__(kET) __attribute__((amdgpu_waves_per_eu(kWavesPerEURep)))
 void k_estep_chunk_rep(const cpg_model model, const uint32_t* __restrict__ packed, int64_t C,
@@ -922,16 +909,10 @@ size_t estep_lds(int lanes, bool rep) {   // the union is sized for 16 waves; fe
 // share the training CUs: the overlapped C2 step (702 chunks) lost 2.5 %, the C3 genome on one
 // GPU (47,303 chunks) gained 7 % (365-372 -> 395-397 Gbase/s; profiles/r04_rep/).  Used from
 // 2,048 chunks (128 Mbp) on: the multi-GPU C3 shards (5,900 chunks at 8 GPUs) and up.
-#ifndef CPG_EST_REP_MIN   // (a build-time override for measurement builds only)
-#define CPG_EST_REP_MIN 2048
-#endif
-constexpr int64_t kEstRepMinChunks = CPG_EST_REP_MIN;
+constexpr int64_t kEstRepMinChunks = 2048;
 // from this many chunks the finalize runs as its own launch (k_train_final): a launch costs
 // ~2-4 us, the last-workgroup protocol ~0.7 us per round of workgroups
-#ifndef CPG_EST_SEPFIN_MIN   // (a build-time override for measurement builds only)
-#define CPG_EST_SEPFIN_MIN 2048
-#endif
-constexpr int64_t kEstSepFinMinChunks = CPG_EST_SEPFIN_MIN;
+constexpr int64_t kEstSepFinMinChunks = 2048;
 unsigned est_rep_grid(int64_t nchunks) { return (unsigned)((nchunks + kRepRun - 1) / kRepRun); }
 }  // namespace
 

@@ -66,6 +66,9 @@ IslWs carve_isl(void* base, int64_t nchunks, int64_t C, int64_t tw) {
     w.toff = (Cnt5*)take(nt * sizeof(Cnt5));
     w.kept = (int32_t*)take(nchunks * maxr * 4);
     w.cres = (int2*)take(nchunks * sizeof(int2));
+    w.cbase = (long long*)take(nchunks * 8);
+    w.bsum = (long long*)take(((nchunks + kBaseBlock - 1) / kBaseBlock) * 8);
+    w.scanned = nchunks > kInlineBaseMax ? 1 : 0;
     w.flags = nullptr;   // WS_IFLG (the fused decode's look-back)
     w.bytes = o + 256;
     return w;
@@ -191,6 +194,58 @@ __global__ __launch_bounds__(kIT) void k_isl_write(const uint32_t* packed, int64
     write_runs(packed, C, ws, o, blockIdx.x, s_part, sk);
 }
 
+// Between the passes, past kInlineBaseMax chunks: every chunk's first record in two launches
+// (O(chunks) work).  k_isl_base: per block of kBaseBlock chunks, the exclusive scan of their
+// kept counts -> cbase, the block's total -> bsum (a block's total < 2^31: a chunk keeps at
+// most chunk_len / 2 islands, 2^19 x 1,024 chunks).  k_isl_bscan: one workgroup, the block
+// totals' exclusive scan in place (int64).
+__global__ __launch_bounds__(kBaseBlock) void k_isl_base(IslWs ws, int64_t nchunks) {
+    __shared__ int32_t sk[kBaseBlock / 64];
+    const int64_t c = (int64_t)blockIdx.x * kBaseBlock + threadIdx.x;
+    const int32_t v = c < nchunks ? ws.cres[c].x : 0;
+    int32_t tot;
+    const int32_t e = wg_scan_sum(v, sk, tot);
+    if (c < nchunks) ws.cbase[c] = e;
+    if (threadIdx.x == 0) ws.bsum[blockIdx.x] = tot;
+}
+__global__ __launch_bounds__(kBaseBlock) void k_isl_bscan(IslWs ws, int64_t nblocks) {
+    __shared__ long long sw[2][kBaseBlock / 64];
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    long long carry = 0;
+    for (int64_t b0 = 0, it = 0; b0 < nblocks; b0 += kBaseBlock, ++it) {
+        const int64_t i = b0 + t;
+        const long long v = i < nblocks ? ws.bsum[i] : 0;
+        long long x = v;
+#pragma unroll
+        for (int off = 1; off < 64; off <<= 1) {
+            const long long y = __shfl_up(x, off);
+            if (lane >= off) x += y;
+        }
+        if (lane == 63) sw[it & 1][wv] = x;   // double-buffered: one barrier per block
+        __syncthreads();
+        long long before = 0, tot = 0;
+        for (int w = 0; w < kBaseBlock / 64; ++w) {
+            const long long s = sw[it & 1][w];
+            before += w < wv ? s : 0;
+            tot += s;
+        }
+        if (i < nblocks) ws.bsum[i] = carry + before + x - v;
+        carry += tot;
+    }
+}
+
+// the two resolve passes (and, past kInlineBaseMax chunks, the base scan between them)
+void launch_resolve(const uint32_t* packed, const IslWs& ws, const IslOut& o, int64_t nchunks,
+                    int64_t C, hipStream_t s) {
+    hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, C, ws, o);
+    if (ws.scanned) {
+        const int64_t nb = (nchunks + kBaseBlock - 1) / kBaseBlock;
+        hipLaunchKernelGGL(k_isl_base, dim3((unsigned)nb), dim3(kBaseBlock), 0, s, ws, nchunks);
+        hipLaunchKernelGGL(k_isl_bscan, dim3(1), dim3(kBaseBlock), 0, s, ws, nb);
+    }
+    hipLaunchKernelGGL(k_isl_write, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, C, ws, o);
+}
+
 }  // namespace
 
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len) {
@@ -232,11 +287,7 @@ hipError_t islands_tiles(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
 }
 hipError_t islands_resolve(const uint32_t* packed, const IslFuse& f, int64_t chunk_len,
                            hipStream_t s) {
-    const int64_t nchunks = f.o.nchunks;
-    hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed,
-                       chunk_len, f.ws, f.o);
-    hipLaunchKernelGGL(k_isl_write, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, chunk_len,
-                       f.ws, f.o);
+    launch_resolve(packed, f.ws, f.o, f.o.nchunks, chunk_len, s);
     return hipGetLastError();
 }
 
@@ -253,10 +304,7 @@ hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t 
     hipLaunchKernelGGL(k_isl_tile, dim3((unsigned)(nchunks * ws.ntile)), dim3(kTT), 0, s, packed,
                        sign, chunk_len, ws);
     const IslOut o{out, cap, count, base_in, first_chunk, 0u, status, nchunks};
-    hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed,
-                       chunk_len, ws, o);
-    hipLaunchKernelGGL(k_isl_write, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, chunk_len,
-                       ws, o);
+    launch_resolve(packed, ws, o, nchunks, chunk_len, s);
     return hipGetLastError();
 }
 

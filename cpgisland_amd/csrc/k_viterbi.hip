@@ -298,14 +298,8 @@ constexpr int kK5WavesPerEU = 8;
 // SIMD — too few to cover a step's table-lookup latency with one another — so its lookups are
 // issued kK5LookFused steps ahead (the registers for them: 2 ahead fits the 64 of 8 waves per
 // SIMD that the long decodes' form keeps)
-#ifndef CPG_K5_LOOK_FUSED
-#define CPG_K5_LOOK_FUSED 4
-#endif
-#ifndef CPG_K5_WPE_FUSED
-#define CPG_K5_WPE_FUSED 6
-#endif
-constexpr int kK5LookFused = CPG_K5_LOOK_FUSED;
-constexpr int kK5WavesPerEUFused = CPG_K5_WPE_FUSED;
+constexpr int kK5LookFused = 4;
+constexpr int kK5WavesPerEUFused = 6;
 __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables* vt) {
     VitDerived* dv = reinterpret_cast<VitDerived*>(vt + 1);
     const int n = kQ4 + kMaxBinade * 16 + kMaxBinade * 64 + kMaxBinade * kW4;

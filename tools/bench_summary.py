@@ -5,6 +5,8 @@ import sys
 d = json.loads(open(sys.argv[1]).read().strip().splitlines()[-1])
 print("value", round(d["value"] / 1e9, 1), "Gbase/s", "ms/step", round(d["ms_per_step"], 4),
       "phases", d.get("phases_ms"))
+print("fingerprint", d.get("fingerprint"))
+print("cold_cache", d.get("cold_cache"))
 for k in ("c3_single_gpu", "bw_iteration"):
     if isinstance(d.get(k), dict):
         v = d[k]
