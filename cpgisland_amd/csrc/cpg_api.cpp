@@ -40,14 +40,6 @@ int ws_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
     return CPG_OK;
 }
 
-uint32_t lookback_epoch() {
-    static std::atomic<uint32_t> ctr{0};
-    for (;;) {
-        const uint32_t e = (++ctr) * 0x9E3779B1u;
-        if (e != 0u && e != 0xFFFFFFFFu) return e;
-    }
-}
-
 int pin_get(cpg_ctx* ctx, int slot, size_t bytes, void** out) {
     Buf& b = ctx->pin[slot];
     if (b.bytes < bytes) {
@@ -255,7 +247,6 @@ int cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags) {
     if ((rc = ws_get(ctx, WS_VIT, vit, &p))) return rc;
     if ((rc = ws_get(ctx, WS_ISL, isl, &p))) return rc;
     if ((rc = ws_get(ctx, WS_VAGG, agg, &p))) return rc;
-    if ((rc = ws_get(ctx, WS_IFLG, per_chunk, &p))) return rc;
     if ((rc = ws_get(ctx, WS_IDONE, per_chunk, &p))) return rc;
     if ((rc = ws_get(ctx, WS_EST, estep_ws_bytes(nt, CPG_TRAIN_CHUNK), &p))) return rc;
     if (flags & CPG_RESERVE_GENERAL) {
@@ -305,19 +296,11 @@ int cpg_sync(cpg_ctx* ctx, void* stream) {
     if (st) {
         CPG_HIP(hipMemsetAsync(ctx->d_status, 0, 4, s));
         CPG_HIP(hipStreamSynchronize(s));
-        if (st & ST_VIT_LOOKBACK)
-            return set_error(CPG_E_DEVICE,
-                             "viterbi: the look-back over a chunk's earlier segments timed out; "
-                             "the decoded path is unusable (status 0x%x)", st);
         if (st & ST_GEN_NOT_SIGN)
             return set_error(CPG_E_UNSUPPORTED,
                              "viterbi (general model): the decoded path visits states that are "
                              "not their position's base (a dead end of zero transitions); sign "
                              "bits cannot carry it: use cpg_viterbi_states_d (status 0x%x)", st);
-        if (st & ST_LOOKBACK_TIMEOUT)
-            return set_error(CPG_E_DEVICE,
-                             "island records: the look-back over earlier chunks' counts timed "
-                             "out; records and count are unusable (status 0x%x)", st);
         if (st == ST_CONTIG_LAYOUT)
             return set_error(CPG_E_INVALID,
                              "contig batch: a contig breaks the layout contract (offset %% 64, "
@@ -416,11 +399,8 @@ int cpg_islands_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_sign
     const int64_t nch = nbases / chunk_len;
     void* ws;
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &ws))) return rc;
-    void* fl;
-    if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nch + 1) * 8, &fl))) return rc;
     CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, 0, ws, ctx->ws[WS_ISL].bytes, d_out,
-                           cap, d_count, ctx->d_status, pick(ctx, stream),
-                           static_cast<unsigned long long*>(fl)));
+                           cap, d_count, pick(ctx, stream)));
     return CPG_OK;
 }
 
@@ -436,11 +416,8 @@ int cpg_islands_at_d(cpg_ctx* ctx, const uint32_t* d_packed, const uint32_t* d_s
     const int64_t nch = nbases / chunk_len;
     void* ws;
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &ws))) return rc;
-    void* fl;
-    if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nch + 1) * 8, &fl))) return rc;
     CPG_HIP(launch_islands(d_packed, d_sign, nch, chunk_len, first_chunk, ws,
-                           ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status,
-                           pick(ctx, stream), static_cast<unsigned long long*>(fl)));
+                           ctx->ws[WS_ISL].bytes, d_out, cap, d_count, pick(ctx, stream)));
     return CPG_OK;
 }
 
@@ -464,8 +441,6 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
     const int64_t ntail = w_all > w_done ? w_all - w_done : 0;
     void* wsi;
     if ((rc = ws_get(ctx, WS_ISL, islands_ws_bytes(nch, chunk_len), &wsi))) return rc;
-    void* fl;
-    if ((rc = ws_get(ctx, WS_IFLG, (size_t)(nch + 1) * 8, &fl))) return rc;
     if (nch == 0) {
         if (ntail) CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)ntail * 4, s));
         CPG_HIP(hipMemsetAsync(d_count, 0, sizeof(int64_t), s));
@@ -481,8 +456,7 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
             return rc;
         if (ntail) CPG_HIP(hipMemsetAsync(d_sign_out + w_done, 0, (size_t)ntail * 4, s));
         CPG_HIP(launch_islands(spk, d_sign_out, nch, chunk_len, first_chunk, wsi,
-                               ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status, s,
-                               static_cast<unsigned long long*>(fl)));
+                               ctx->ws[WS_ISL].bytes, d_out, cap, d_count, s));
         return CPG_OK;
     }
     VitConsts vc;
@@ -498,16 +472,16 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
     if ((rc = ws_get(ctx, WS_IDONE, (size_t)nch * 8, &dn))) return rc;
     unsigned int* done = static_cast<unsigned int*>(dn);
     // fused: the traceback writes the island run records and a chunk's last traceback
-    // workgroup resolves it — no island kernels
+    // workgroup runs its first resolve pass; the write pass places the records after it
     if (islands_fusable(nch, chunk_len) && tail_fusion_pays(nch)) {
         IslFuse fz;
         CPG_HIP(islands_fuse(&fz, wsi, ctx->ws[WS_ISL].bytes, nch, chunk_len, first_chunk, d_out,
-                             cap, d_count, ctx->d_status, static_cast<unsigned long long*>(fl),
-                             done + nch));
+                             cap, d_count, done + nch));
         CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
                                d_sign_out, d_score, nullptr, ctx->d_status, s,
                                static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,
                                &fz, done));
+        CPG_HIP(islands_write(d_packed, fz, chunk_len, s));
         return CPG_OK;
     }
     if (islands_fusable(nch, chunk_len)) {
@@ -515,7 +489,7 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
         // signs are not read again), the two resolve passes run after it
         IslFuse fz;
         CPG_HIP(islands_tiles(&fz, wsi, ctx->ws[WS_ISL].bytes, nch, chunk_len, first_chunk, d_out,
-                              cap, d_count, ctx->d_status));
+                              cap, d_count));
         CPG_HIP(launch_viterbi(vc, d_vt, d_packed, nch, chunk_len, ws, ctx->ws[WS_VIT].bytes,
                                d_sign_out, d_score, nullptr, ctx->d_status, s,
                                static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,
@@ -528,8 +502,7 @@ int cpg_decode_d(cpg_ctx* ctx, const cpg_model* model, const uint32_t* d_packed,
                            static_cast<unsigned long long*>(agg), d_sign_out + w_done, ntail,
                            nullptr, done));
     CPG_HIP(launch_islands(d_packed, d_sign_out, nch, chunk_len, first_chunk, wsi,
-                           ctx->ws[WS_ISL].bytes, d_out, cap, d_count, ctx->d_status, s,
-                           static_cast<unsigned long long*>(fl)));
+                           ctx->ws[WS_ISL].bytes, d_out, cap, d_count, s));
     return CPG_OK;
 }
 

@@ -31,8 +31,8 @@ enum : uint32_t {
     ST_VERIFY_MAG = 1u << 1,     // K3 composite outside the exact range
     ST_VERIFY_CHAIN = 1u << 2,   // K7 traceback start state mismatch
     ST_CONTIG_LAYOUT = 1u << 3,  // a contig breaks the batch layout contract (skipped)
-    ST_LOOKBACK_TIMEOUT = 1u << 4,   // a bounded look-back spin gave up (records unusable)
-    ST_VIT_LOOKBACK = 1u << 5,       // the Viterbi segment look-back gave up (path unusable)
+    // (bits 4 and 5 reported the bounded look-back spins of rounds 2-5: no kernel waits for
+    // another workgroup any more)
     ST_GEN_NOT_SIGN = 1u << 6,       // general-model path: a state is not its base's (the path
                                      // is not representable as sign bits)
 };
@@ -144,18 +144,14 @@ struct Buf {
 enum { WS_COUNT = 0, WS_VIT = 1, WS_ISL = 2, WS_EST = 3, WS_IN0 = 4, WS_IN1 = 5, WS_OUT0 = 6,
        WS_OUT1 = 7, WS_OUT2 = 8, WS_ING = 9, WS_GEN = 10, WS_GISL = 11, WS_CSORT = 12,
        WS_CBP = 13, WS_CISL = 14, WS_CCK = 15,
-       // look-back words tagged with a per-call epoch (Viterbi segment products, island
-       // counts): slots of their own, so that stale words are only older tags — never other
-       // arrays of a differently laid-out earlier call whose bits could pass for the tag
-       WS_VAGG = 16, WS_IFLG = 17,
+       // K1's segment products (read by the next launch, k_vit_segplan); 17: unused (the
+       // island look-back flags of rounds 2-5)
+       WS_VAGG = 16,
        // per-chunk done counters of the fused decode: zero between calls (zero-filled when
        // allocated, reset by the workgroup that completes a chunk), so a slot of their own
        WS_IDONE = 18,
        // the general-model Viterbi (backpointer ballots, states, state-packed words)
        WS_VGEN = 19, WS_NSLOT = 20 };
-// a fresh look-back tag per call: an odd multiple of a counter (a bijection: distinct for 2^32
-// calls), never 0 (zero-filled workspace) or all ones
-uint32_t lookback_epoch();
 
 }  // namespace cpg
 
@@ -235,12 +231,12 @@ hipError_t launch_vit_tables(const VitConsts& vc, VitTables* d_vt, hipStream_t s
 int64_t vit_nsb(int64_t chunk_len);
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* ws, size_t ws_bytes,
-                          cpg_island* out, int64_t cap, int64_t* count, uint32_t* status,
-                          hipStream_t s, unsigned long long* flags,
-                          const int64_t* base_in = nullptr);   // flags: WS_IFLG, nchunks words
+                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s,
+                          const int64_t* base_in = nullptr);
 size_t islands_ws_bytes(int64_t nchunks, int64_t chunk_len);
 // fused decode (cpg_decode_d): the traceback writes the island tile lists and a chunk's last
-// traceback workgroup resolves it (no island kernels); done: nchunks zeroed words (WS_IDONE)
+// traceback workgroup runs the chunk's first resolve pass (done: nchunks zeroed words,
+// WS_IDONE); islands_write places the records after it (no island tile / resolve kernels)
 bool islands_fusable(int64_t nchunks, int64_t chunk_len);
 // Per-chunk tail work folded into the last workgroup of a chunk (K6 into K5, the island tiles
 // and the chunk resolve into K7) pays while the chunks are few: it saves a launch and the
@@ -254,13 +250,14 @@ constexpr int64_t kTailFuseMaxChunks = 256;
 inline bool tail_fusion_pays(int64_t nchunks) { return nchunks <= kTailFuseMaxChunks; }
 hipError_t islands_fuse(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
                         int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
-                        int64_t* count, uint32_t* status, unsigned long long* flags,
-                        unsigned int* done, const int64_t* base_in = nullptr);
+                        int64_t* count, unsigned int* done, const int64_t* base_in = nullptr);
+hipError_t islands_write(const uint32_t* packed, const IslFuse& f, int64_t chunk_len,
+                         hipStream_t s);
 // the fused decode past kTailFuseMaxChunks chunks: the traceback writes the island tiles
-// (IslFuse with done == null) and islands_resolve places the records after it
+// (IslFuse with done == null) and islands_resolve runs both resolve passes after it
 hipError_t islands_tiles(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
                          int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
-                         int64_t* count, uint32_t* status, const int64_t* base_in = nullptr);
+                         int64_t* count, const int64_t* base_in = nullptr);
 hipError_t islands_resolve(const uint32_t* packed, const IslFuse& f, int64_t chunk_len,
                            hipStream_t s);
 // gtab: the model's one-step tables in device memory (est_tables); needed with PART_ACC

@@ -124,9 +124,8 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
     if (estep_out && (rc = est_tables(ctx, train_model, &est_gtab))) return rc;
     if (decode && (rc = ws_get(ctx, WS_VIT, viterbi_ws_bytes(wdec, D), &ws_vit))) return rc;
     if (decode && (rc = ws_get(ctx, WS_ISL, islands_ws_bytes(wdec, D), &ws_isl))) return rc;
-    void *ws_agg = nullptr, *ws_fl = nullptr, *ws_done = nullptr;
+    void *ws_agg = nullptr, *ws_done = nullptr;
     if (decode && (rc = ws_get(ctx, WS_VAGG, viterbi_agg_bytes(wdec, D), &ws_agg))) return rc;
-    if (decode && (rc = ws_get(ctx, WS_IFLG, (size_t)(wdec + 1) * 8, &ws_fl))) return rc;
     if (decode && (rc = ws_get(ctx, WS_IDONE, (size_t)(wdec + 1) * 8, &ws_done))) return rc;
     // window buffers + results, one allocation
     const size_t bp = up256((size_t)(W / 16) * 4 + 64), bs = up256((size_t)(W / 32) * 4 + 64);
@@ -198,13 +197,13 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
                     IslFuse fz;
                     CPG_HIP(islands_fuse(&fz, ws_isl, ctx->ws[WS_ISL].bytes, nd, D,
                                          chunk0 + start / D, d_isl, island_cap, d_icnt + k + 1,
-                                         ctx->d_status, static_cast<unsigned long long*>(ws_fl),
                                          static_cast<unsigned int*>(ws_done) + nd, d_icnt + k));
                     CPG_HIP(launch_viterbi(vc, d_vt, buf_packed(b), nd, D, ws_vit,
                                            ctx->ws[WS_VIT].bytes, buf_out(b), d_score + start / D,
                                            nullptr, ctx->d_status, sdec,
                                            static_cast<unsigned long long*>(ws_agg), nullptr, 0,
                                            &fz, static_cast<unsigned int*>(ws_done)));
+                    CPG_HIP(islands_write(buf_packed(b), fz, D, sdec));
                 } else {
                     CPG_HIP(launch_viterbi(vc, d_vt, buf_packed(b), nd, D, ws_vit,
                                            ctx->ws[WS_VIT].bytes, buf_out(b), d_score + start / D,
@@ -213,8 +212,7 @@ extern "C" int cpg_genome_run(cpg_ctx* ctx, const cpg_model* train_model,
                                            nullptr, static_cast<unsigned int*>(ws_done)));
                     CPG_HIP(launch_islands(buf_packed(b), buf_out(b), nd, D, chunk0 + start / D,
                                            ws_isl, ctx->ws[WS_ISL].bytes, d_isl, island_cap,
-                                           d_icnt + k + 1, ctx->d_status, sdec,
-                                           static_cast<unsigned long long*>(ws_fl), d_icnt + k));
+                                           d_icnt + k + 1, sdec, d_icnt + k));
                 }
             } else {
                 CPG_HIP(hipMemcpyAsync(d_icnt + k + 1, d_icnt + k, 8, hipMemcpyDeviceToDevice, sdec));

@@ -114,9 +114,8 @@ struct IslWs {
     Cnt5* ttot;         // per tile: totals (kernel T)
     Cnt5* toff;         // per tile: exclusive prefix in its chunk (kernel R)
     int32_t* kept;      // per chunk, maxr: rank*2 | stale_in, or -1
-    unsigned long long* flags;   // per chunk: epoch << 32 | kept islands (look-back)
-    // the two-pass resolve (separate island kernels: no look-back): per chunk {kept islands,
-    // closed runs}; per run its kept[] word (stale_in, or -1: filtered out)
+    // the two-pass resolve (no look-back): per chunk {kept islands, closed runs}; per run its
+    // kept[] word (stale_in, or -1: filtered out)
     int2* cres;
     // past kInlineBaseMax chunks (the split path): every chunk's first record, scanned once
     // from cres between the two passes (k_isl_base: per block of 1,024 chunks -> cbase and the
@@ -294,8 +293,6 @@ struct IslOut {
     int64_t* count;            // total records (with base_in)
     const int64_t* base_in;    // append mode: records already written before this call
     int64_t first_chunk;
-    uint32_t epoch;            // tags this call's look-back flags
-    uint32_t* status;          // ctx status word: ST_LOOKBACK_TIMEOUT when a spin gives up
     int64_t nchunks;           // the last chunk writes the count
 };
 
@@ -313,69 +310,17 @@ __device__ __forceinline__ void put_island(const IslOut& o, const RunStat& rs, u
     o.out[dst] = isl;
 }
 
-// kept islands of the chunks before c: a decoupled look-back over their flags (this call's
-// epoch).  A chunk publishes its own count first (an aggregate), then, once it knows the
-// count before it, its inclusive prefix (bit 31 set): a look-back reads windows of 64
-// chunks (one wave), and stops at the nearest inclusive prefix, so a chunk walks back over
-// the few chunks still in flight instead of every chunk before it (O(chunks) per chunk had
-// made the island resolve 210 us at 2,956 chunks).  Workgroups start in chunk order, so
-// every chunk waited on is running or done; the spin is bounded all the same (2 s of wall
-// clock).  A spin that gives up sets ST_LOOKBACK_TIMEOUT in the status word (cpg_sync then
-// fails the call: the offsets, and so every record and the count, are unusable) and counts
-// nothing for that chunk.  CPG_ISL_SPIN_LIMIT (ticks of the 100 MHz wall clock) is a test
-// hook.  Counts stay below 2^31 (islands of one call).
-#ifndef CPG_ISL_SPIN_LIMIT
-#define CPG_ISL_SPIN_LIMIT 200000000ull
-#endif
-constexpr uint32_t kInclusive = 0x80000000u;
-__device__ __forceinline__ long long kept_before(const IslWs& ws, int64_t c, uint32_t epoch,
-                                                 uint32_t* status) {
-    const int lane = threadIdx.x & 63;
-    long long sum = 0;
-    bool gave_up = false;
-    const unsigned long long t0 = wall_clock64();
-    for (int64_t j0 = c - 1; j0 >= 0; j0 -= 64) {
-        const int64_t j = j0 - lane;   // lane 0: the nearest chunk of the window
-        uint32_t v = 0u;
-        if (j >= 0) {
-            unsigned long long f;
-            for (;;) {
-                // deadline first: a limit of 0 gives up deterministically (the test hook)
-                if (wall_clock64() - t0 >= (unsigned long long)(CPG_ISL_SPIN_LIMIT)) {
-                    gave_up = true;
-                    f = 0;
-                    break;
-                }
-                f = __hip_atomic_load(ws.flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                if ((uint32_t)(f >> 32) == epoch) break;
-                __builtin_amdgcn_s_sleep(1);
-            }
-            v = (uint32_t)f;
-        }
-        // the nearest inclusive prefix of the window: lanes up to it add, the rest do not
-        const unsigned long long inc = __ballot(j >= 0 && (v & kInclusive));
-        const int stop = inc ? (int)__builtin_ctzll(inc) : 64;
-        if (lane <= stop) sum += (long long)(v & ~kInclusive);
-        if (inc) break;   // wave-uniform
-    }
-    if (gave_up) atomicOr(status, ST_LOOKBACK_TIMEOUT);
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) sum += __shfl_xor(sum, off);
-    return sum;
-}
-
-// the chunk's closed runs split over the lanes: stale-atC maps composed and scanned,
-// filtered (:280-285), kept islands ranked, the chunk's first record found by the look-back,
-// records written.  With <= 8 runs per lane the map and both filter outcomes (stale 0 / 1)
-// of each run stay in registers: one pass of loads before the records.
-// kSplit (the separate kernels' first pass, no look-back): every run's kept[] word (stale_in,
-// or -1: filtered out) and the chunk's {kept islands, closed runs} in ws.cres; write_runs (the
-// second pass) re-ranks from those and places the records once every chunk's count is known.
-template <bool kAgent, bool kAgentRec, bool kSplit = false>
+// The first pass of a chunk's resolve (k_isl_resolve, or the chunk's last traceback workgroup
+// in a fused decode): the chunk's closed runs split over the lanes, stale-atC maps composed
+// and scanned, filtered (:280-285); every run's kept[] word (stale_in, or -1: filtered out)
+// and the chunk's {kept islands, closed runs} in ws.cres.  The records are placed by the
+// second pass (write_runs, a later kernel) once every chunk's count is known: no workgroup
+// waits for another.  With <= 8 runs per lane the map and both filter outcomes (stale 0 / 1)
+// of each run stay in registers: one pass of loads.
+template <bool kAgent, bool kAgentRec>
 __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws, const Cnt5* to,
-                                             int64_t c, int64_t C, int64_t nr, int32_t* kept,
-                                             uint32_t* sm, int32_t* sk, long long* sbase,
-                                             const IslOut& o) {
+                                             int64_t c, int64_t nr, int32_t* kept, uint32_t* sm,
+                                             int32_t* sk) {
     const int t = threadIdx.x, nl = blockDim.x;
     const int64_t per = (nr + nl - 1) / nl;
     const int64_t r0 = min((int64_t)t * per, nr), r1 = min(r0 + per, nr);
@@ -383,10 +328,8 @@ __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws
     const bool cached = per <= kCache;   // uniform
     uint32_t bits = 0;   // run j: bits 4j.. = map | keep(stale 0) << 2 | keep(stale 1) << 3
     uint32_t F = 0x2u;
-    RunStat rs0{};       // the lane's first run, kept for its record (no second round of loads)
     for (int64_t r = r0; r < r1; ++r) {
         const RunStat rs = run_stat<kAgent, kAgentRec>(pk, ws, to, c, r);
-        if (r == r0) rs0 = rs;
         const uint32_t m = stale_map(rs);
         F = mcompose(m, F);
         if (cached)
@@ -399,7 +342,9 @@ __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws
     if (cached) {
         for (int64_t j = 0; j < r1 - r0; ++j) {
             const uint32_t b = bits >> (4 * j);
-            nk += (b >> (2 + stale)) & 1u;
+            const bool keep = (b >> (2 + stale)) & 1u;
+            kept[r0 + j] = keep ? (int32_t)stale : -1;
+            nk += keep;
             stale = mapply(b & 3u, stale);
         }
     } else {
@@ -412,56 +357,8 @@ __device__ __forceinline__ void resolve_runs(const uint32_t* pk, const IslWs& ws
         }
     }
     int32_t nkt;
-    int32_t rank = wg_scan_sum(nk, sk, nkt);
-    if constexpr (kSplit) {   // every run's kept[] word for write_runs (cached: from the bits)
-        if (cached) {
-            uint32_t st = stale0;
-            for (int64_t j = 0; j < r1 - r0; ++j) {
-                const uint32_t b = bits >> (4 * j);
-                kept[r0 + j] = ((b >> (2 + st)) & 1u) ? (int32_t)st : -1;
-                st = mapply(b & 3u, st);
-            }
-        }
-        if (t == 0) ws.cres[c] = make_int2(nkt, (int32_t)nr);
-        return;
-    }
-    // publish this chunk's count, then find the kept islands of the chunks before it
-    if (t == 0)
-        __hip_atomic_store(ws.flags + c, ((unsigned long long)o.epoch << 32) | (uint32_t)nkt,
-                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    if (t < 64) {
-        const long long before = kept_before(ws, c, o.epoch, o.status);
-        // the flag word holds 31 bits of prefix: a call with 2^31 islands or more cannot be
-        // placed — report it as a failed look-back instead of wrapping silently
-        if (t == 0 && before + nkt >= (long long)kInclusive) atomicOr(o.status, ST_LOOKBACK_TIMEOUT);
-        if (t == 0) {
-            *sbase = before;
-            __hip_atomic_store(ws.flags + c,
-                               ((unsigned long long)o.epoch << 32) | kInclusive |
-                                   (uint32_t)(before + nkt),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
-    }
-    __syncthreads();
-    const int64_t base = *sbase + (o.base_in ? *o.base_in : 0);
-    if (c == o.nchunks - 1 && t == 0) *o.count = base + nkt;
-    const int64_t gchunk = o.first_chunk + c;
-    const uint32_t cbase = (uint32_t)gchunk * (uint32_t)C;   // chunk*0x100000, Java int
-    if (cached) {
-        stale = stale0;
-        for (int64_t j = 0; j < r1 - r0; ++j) {
-            const uint32_t b = bits >> (4 * j);
-            if ((b >> (2 + stale)) & 1u)
-                put_island(o, j == 0 ? rs0 : run_stat<kAgent, kAgentRec>(pk, ws, to, c, r0 + j), stale,
-                           base + rank++, gchunk, cbase);
-            stale = mapply(b & 3u, stale);
-        }
-    } else {
-        for (int64_t r = r0; r < r1; ++r)
-            if (kept[r] >= 0)
-                put_island(o, run_stat<kAgent, kAgentRec>(pk, ws, to, c, r), (uint32_t)(kept[r] & 1),
-                           base + rank++, gchunk, cbase);
-    }
+    (void)wg_scan_sum(nk, sk, nkt);
+    if (t == 0) ws.cres[c] = make_int2(nkt, (int32_t)nr);
 }
 
 
@@ -497,17 +394,16 @@ struct ResolveLds {
     Cnt5 s5[2][16];
     uint32_t sm[16];
     int32_t sk[16];
-    long long sbase;
 };
 
 // The per-chunk resolve (kernel R, or the last traceback workgroup of a chunk in a fused
 // decode): tile offsets (exclusive scan of the chunk's tile totals in blocks of blockDim.x
-// tiles; in LDS `s_to` for up to kToff tiles, else in ws.toff), then resolve_runs.
-// kAgentRec: the tile lists and totals were written by other workgroups of this kernel.
-template <bool kAgentRec, int kToff, bool kSplit = false>
+// tiles; kept in LDS `s_to` for up to kToff tiles for the runs' stats, and written to ws.toff
+// for the second pass), then resolve_runs.  kAgentRec: the tile lists and totals were written
+// by other workgroups of this kernel.
+template <bool kAgentRec, int kToff>
 __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C, const IslWs& ws,
-                                              const IslOut& o, int64_t c, ResolveLds& L,
-                                              Cnt5* s_to) {
+                                              int64_t c, ResolveLds& L, Cnt5* s_to) {
     const int t = threadIdx.x, nl = blockDim.x;
     const int64_t maxr = C / 2 + 1;
     const uint32_t* pk = packed + c * (C / 16);
@@ -522,8 +418,7 @@ __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C,
         if (i < ws.ntile) {
             const Cnt5 oo = cadd(e, carry);
             if (in_lds) s_to[i] = oo;
-            // (kSplit: write_runs, the next kernel, reads the offsets from ws.toff)
-            if (!in_lds || kSplit) ws.toff[c * ws.ntile + i] = oo;
+            ws.toff[c * ws.ntile + i] = oo;   // (write_runs, the next kernel, reads them here)
         }
         carry = cadd(carry, tot);
     }
@@ -533,10 +428,9 @@ __device__ __forceinline__ void resolve_chunk(const uint32_t* packed, int64_t C,
     const int64_t nr = carry.cl;
     int32_t* kept = ws.kept + c * maxr;
     if (in_lds)
-        resolve_runs<false, kAgentRec, kSplit>(pk, ws, s_to, c, C, nr, kept, L.sm, L.sk, &L.sbase, o);
+        resolve_runs<false, kAgentRec>(pk, ws, s_to, c, nr, kept, L.sm, L.sk);
     else
-        resolve_runs<true, kAgentRec, kSplit>(pk, ws, ws.toff + c * ws.ntile, c, C, nr, kept, L.sm,
-                                              L.sk, &L.sbase, o);
+        resolve_runs<true, kAgentRec>(pk, ws, ws.toff + c * ws.ntile, c, nr, kept, L.sm, L.sk);
 }
 
 // The second pass of the two-pass resolve: chunk c's first record = the kept islands of the

@@ -22,8 +22,8 @@
 //   W (per chunk): the chunk's first record = the kept counts of the chunks before it (summed
 //     from R's per-chunk counts: a kernel boundary instead of a look-back, so no workgroup
 //     ever waits for another), island records.
-// (The fused decode, k_viterbi.hip, resolves a chunk in its last traceback workgroup and finds
-// the chunk's first record by a decoupled look-back over the earlier chunks' flags.)
+// (The fused decode, k_viterbi.hip, runs R for a chunk in its last traceback workgroup; W
+// runs after the traceback.)
 // A whole chunk per workgroup would stream at one CU's share of the memory system (≈25-70
 // GB/s per CU): the tiles spread the one pass over the data on every CU.
 
@@ -69,7 +69,6 @@ IslWs carve_isl(void* base, int64_t nchunks, int64_t C, int64_t tw) {
     w.cbase = (long long*)take(nchunks * 8);
     w.bsum = (long long*)take(((nchunks + kBaseBlock - 1) / kBaseBlock) * 8);
     w.scanned = nchunks > kInlineBaseMax ? 1 : 0;
-    w.flags = nullptr;   // WS_IFLG (the fused decode's look-back)
     w.bytes = o + 256;
     return w;
 }
@@ -178,14 +177,14 @@ __global__ __launch_bounds__(kTT) void k_isl_tile(const uint32_t* packed, const 
 }
 
 // R, two passes (no workgroup waits for another: two processes' decodes may share a GPU):
-// the per-chunk resolve up to the kept ranks (resolve_chunk<kSplit>), then the records
+// the per-chunk resolve up to the kept words and counts (resolve_chunk), then the records
 // (write_runs) once every chunk's kept count is in ws.cres
 constexpr int kToffLds = 1024;
 __global__ __launch_bounds__(kIT) void k_isl_resolve(const uint32_t* packed, int64_t C,
-                                                    IslWs ws, IslOut o) {
+                                                    IslWs ws) {
     __shared__ ResolveLds L;
     __shared__ Cnt5 s_to[kToffLds];
-    resolve_chunk<false, kToffLds, true>(packed, C, ws, o, blockIdx.x, L, s_to);
+    resolve_chunk<false, kToffLds>(packed, C, ws, blockIdx.x, L, s_to);
 }
 __global__ __launch_bounds__(kIT) void k_isl_write(const uint32_t* packed, int64_t C, IslWs ws,
                                                   IslOut o) {
@@ -234,16 +233,21 @@ __global__ __launch_bounds__(kBaseBlock) void k_isl_bscan(IslWs ws, int64_t nblo
     }
 }
 
-// the two resolve passes (and, past kInlineBaseMax chunks, the base scan between them)
-void launch_resolve(const uint32_t* packed, const IslWs& ws, const IslOut& o, int64_t nchunks,
-                    int64_t C, hipStream_t s) {
-    hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, C, ws, o);
+// the second pass (and, past kInlineBaseMax chunks, the base scan before it)
+void launch_write(const uint32_t* packed, const IslWs& ws, const IslOut& o, int64_t nchunks,
+                  int64_t C, hipStream_t s) {
     if (ws.scanned) {
         const int64_t nb = (nchunks + kBaseBlock - 1) / kBaseBlock;
         hipLaunchKernelGGL(k_isl_base, dim3((unsigned)nb), dim3(kBaseBlock), 0, s, ws, nchunks);
         hipLaunchKernelGGL(k_isl_bscan, dim3(1), dim3(kBaseBlock), 0, s, ws, nb);
     }
     hipLaunchKernelGGL(k_isl_write, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, C, ws, o);
+}
+// both resolve passes
+void launch_resolve(const uint32_t* packed, const IslWs& ws, const IslOut& o, int64_t nchunks,
+                    int64_t C, hipStream_t s) {
+    hipLaunchKernelGGL(k_isl_resolve, dim3((unsigned)nchunks), dim3(kIT), 0, s, packed, C, ws);
+    launch_write(packed, ws, o, nchunks, C, s);
 }
 
 }  // namespace
@@ -262,26 +266,30 @@ bool islands_fusable(int64_t nchunks, int64_t chunk_len) {
 
 hipError_t islands_fuse(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
                         int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
-                        int64_t* count, uint32_t* status, unsigned long long* flags,
-                        unsigned int* done, const int64_t* base_in) {
-    if (!islands_fusable(nchunks, chunk_len) || !flags || !done) return hipErrorInvalidValue;
+                        int64_t* count, unsigned int* done, const int64_t* base_in) {
+    if (!islands_fusable(nchunks, chunk_len) || !done) return hipErrorInvalidValue;
     f->ws = carve_isl(ws, nchunks, chunk_len, kFTW);
     if (f->ws.bytes > ws_bytes) return hipErrorInvalidValue;
-    f->ws.flags = flags;
-    f->o = IslOut{out, cap, count, base_in, first_chunk, lookback_epoch(), status, nchunks};
+    f->o = IslOut{out, cap, count, base_in, first_chunk, nchunks};
     f->done = done;
     return hipSuccess;
+}
+// the records of a fused decode whose traceback resolved every chunk (first pass)
+hipError_t islands_write(const uint32_t* packed, const IslFuse& f, int64_t chunk_len,
+                         hipStream_t s) {
+    launch_write(packed, f.ws, f.o, f.o.nchunks, chunk_len, s);
+    return hipGetLastError();
 }
 
 // past 256 chunks the fused decode's traceback writes the tiles (kFTW, plain stores: f->done
 // stays null) and islands_resolve runs the two resolve passes after it
 hipError_t islands_tiles(IslFuse* f, void* ws, size_t ws_bytes, int64_t nchunks,
                          int64_t chunk_len, int64_t first_chunk, cpg_island* out, int64_t cap,
-                         int64_t* count, uint32_t* status, const int64_t* base_in) {
+                         int64_t* count, const int64_t* base_in) {
     if (!islands_fusable(nchunks, chunk_len)) return hipErrorInvalidValue;
     f->ws = carve_isl(ws, nchunks, chunk_len, kFTW);
     if (f->ws.bytes > ws_bytes) return hipErrorInvalidValue;
-    f->o = IslOut{out, cap, count, base_in, first_chunk, 0u, status, nchunks};
+    f->o = IslOut{out, cap, count, base_in, first_chunk, nchunks};
     f->done = nullptr;
     return hipSuccess;
 }
@@ -293,17 +301,16 @@ hipError_t islands_resolve(const uint32_t* packed, const IslFuse& f, int64_t chu
 
 hipError_t launch_islands(const uint32_t* packed, const uint32_t* sign, int64_t nchunks,
                           int64_t chunk_len, int64_t first_chunk, void* wsp, size_t ws_bytes,
-                          cpg_island* out, int64_t cap, int64_t* count, uint32_t* status,
-                          hipStream_t s, unsigned long long* flags, const int64_t* base_in) {
+                          cpg_island* out, int64_t cap, int64_t* count, hipStream_t s,
+                          const int64_t* base_in) {
     IslWs ws = carve_isl(wsp, nchunks, chunk_len, kTW);
     if (ws.bytes > ws_bytes) return hipErrorInvalidValue;
-    (void)flags;   // the separate kernels need no look-back flags
     if (nchunks == 0)
         return base_in ? hipMemcpyAsync(count, base_in, sizeof(int64_t), hipMemcpyDeviceToDevice, s)
                        : hipMemsetAsync(count, 0, sizeof(int64_t), s);
     hipLaunchKernelGGL(k_isl_tile, dim3((unsigned)(nchunks * ws.ntile)), dim3(kTT), 0, s, packed,
                        sign, chunk_len, ws);
-    const IslOut o{out, cap, count, base_in, first_chunk, 0u, status, nchunks};
+    const IslOut o{out, cap, count, base_in, first_chunk, nchunks};
     launch_resolve(packed, ws, o, nchunks, chunk_len, s);
     return hipGetLastError();
 }

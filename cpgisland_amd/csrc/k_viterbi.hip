@@ -345,27 +345,18 @@ __global__ __launch_bounds__(kThreads) void k_vit_tables(VitConsts vc, VitTables
     }
 }
 
-// Segment path of K1 (chunks of whole 256-block segments): K2's work folded in.  Each
-// workgroup (one segment) scans its blocks' approximate composites, publishes the segment's
-// product as 8 epoch-tagged 64-bit words (no fence needed: every word validates itself),
-// multiplies the products of the chunk's earlier segments (a look-back: workgroups start in
-// order, so every segment waited on is running or done; the spin is bounded) into its entry
-// estimate, and classifies its own blocks.  Irregular blocks go to a per-segment list.
+// Segment path of K1 (chunks of whole 256-block segments): each workgroup (one segment) also
+// stores its segment's ordered product of the approximate composites; the next launch,
+// k_vit_segplan (K2's work per segment), reads the products of the chunk's earlier segments
+// from it — a kernel boundary, so no workgroup waits for another.
 struct ApproxSeg {
-    unsigned long long* agg;   // [segment][8]: epoch << 32 | 32-bit half of the product
-    uint32_t epoch;
+    CI* segprod;               // [segment]: product of the segment's block composites (K1)
     longlong2* aent;
     uint8_t* degen;
     VitPlan* plan;
     int32_t* irrlist;          // [segment][256]
     int32_t* irrseg;           // [segment]: irregular blocks listed
-    uint32_t* status;
 };
-#ifndef CPG_VIT_SPIN_LIMIT
-#define CPG_VIT_SPIN_LIMIT 200000000ull   // 2 s of the 100 MHz wall clock
-#endif
-__device__ void approx_segment(const VitConsts& vc, const Geo& g, const uint32_t* pk, int64_t c,
-                               int64_t k, CI x, const ApproxSeg& as);
 __device__ __forceinline__ int64_t fix_of(double x, int f);
 __device__ __forceinline__ VitPlan classify(const VitConsts& vc, const Geo& g, int64_t k,
                                             longlong2 en, longlong2 ex, bool& irregular);
@@ -402,11 +393,24 @@ __global__ __launch_bounds__(kThreads) void k_vit_approx(VitConsts vc, const uin
                 return (j == 0 && first) ? 1024u + (wi >> 2) : wi;
             },
             [&](uint32_t wi) { return Q4[wi]; }, [&](const int4 q, int) { acc = i4_mul(acc, q); });
-        if (as.agg) {   // segment path (whole blocks only)
-            approx_segment(vc, g, pk, c, k, CI{acc.x, acc.y, acc.z, acc.w}, as);
-            return;
-        }
         comp[gid] = acc;
+        if (as.segprod) {   // segment path (whole blocks only): the segment's ordered product,
+                            // a butterfly over the wave (the lower lane's factor first), then
+                            // the four wave products in order
+            CI x{acc.x, acc.y, acc.z, acc.w};
+            const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const CI y{__shfl_xor(x.pp, off), __shfl_xor(x.pm, off), __shfl_xor(x.mp, off),
+                           __shfl_xor(x.mm, off)};
+                x = (lane & off) ? ci_mul(y, x) : ci_mul(x, y);
+            }
+            __shared__ CI sW[kThreads / 64];
+            if (lane == 0) sW[wv] = x;
+            __syncthreads();
+            if (threadIdx.x == 0)
+                as.segprod[blockIdx.x] = ci_mul(ci_mul(sW[0], sW[1]), ci_mul(sW[2], sW[3]));
+        }
         return;
     }
     int32_t a = 0, b = kNeg32, e = kNeg32, f = 0;
@@ -551,14 +555,20 @@ __global__ __launch_bounds__(kScanT) void k_vit_scan(VitConsts vc, const uint32_
     if (t == 0) irrcount[c] = sIrr;
 }
 
-// K1's segment path after the block composite x (see ApproxSeg)
-__device__ void approx_segment(const VitConsts& vc, const Geo& g, const uint32_t* pk, int64_t c,
-                               int64_t k, CI x, const ApproxSeg& as) {
+// K2 of the segment path, one workgroup per segment: the segment's entry estimate (the chunk's
+// start times the products of its earlier segments, stored by K1), the exclusive scan of its
+// blocks' composites (exact integer max-plus), the classification of its blocks; irregular
+// blocks go to the segment's list.
+__global__ __launch_bounds__(kThreads) void k_vit_segplan(VitConsts vc, const uint32_t* packed,
+                                                          Geo g, const int4* __restrict__ comp,
+                                                          ApproxSeg as) {
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t gid = (int64_t)blockIdx.x * kThreads + t;
+    const int64_t c = gid / g.nsb, k = gid - c * g.nsb;
     const int sidx = (int)(k / kThreads);   // segment within the chunk (workgroup-uniform)
+    const uint32_t* pk = chunk_ptr(packed, g, c);
     const uint32_t o0 = base_at(pk, 0);
     const double lp = vc.logpi[o0], lm = vc.logpi[o0 + 4];
-    const int64_t gid = (int64_t)blockIdx.x * kThreads + t;
     if (!(lp > -INFINITY) && !(lm > -INFINITY)) {   // DEGEN chunk (uniform)
         as.plan[gid] = VitPlan{PLAN_DEGEN, 0, 0, 0, 0, 0};
         if (t == 0) {
@@ -568,17 +578,20 @@ __device__ void approx_segment(const VitConsts& vc, const Geo& g, const uint32_t
         return;
     }
     if (t == 0 && sidx == 0) as.degen[c] = 0;
-    // inclusive scan of the segment's composites (exact integer max-plus)
+    const int4 x4 = comp[gid];
+    const CI x{x4.x, x4.y, x4.z, x4.w};
+    __shared__ CI sPre[kMaxSeg];
+    __shared__ CI sW[kThreads / 64];
+    __shared__ longlong2 sEnt;
+    __shared__ int sIrr;
+    if (t < sidx) sPre[t] = as.segprod[(int64_t)blockIdx.x - sidx + t];
+    // inclusive scan of the segment's composites
     CI s = x;
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
         const CI y = shfl_up_ci(s, off);
         if (lane >= off) s = ci_mul(y, s);
     }
-    __shared__ CI sW[kThreads / 64];
-    __shared__ unsigned long long sPre[16 * 8];
-    __shared__ longlong2 sEnt;
-    __shared__ int sIrr;
     if (lane == 63) sW[wv] = s;
     if (t == 0) sIrr = 0;
     __syncthreads();
@@ -586,43 +599,10 @@ __device__ void approx_segment(const VitConsts& vc, const Geo& g, const uint32_t
     for (int w = 0; w < wv; ++w) before = ci_mul(before, sW[w]);
     const CI up = shfl_up_ci(s, 1);
     const CI excl = lane > 0 ? ci_mul(before, up) : before;
-    // publish the segment's product, then read the earlier segments' (this call's epoch)
-    if (t < 8) {
-        const CI tot = ci_mul(ci_mul(sW[0], sW[1]), ci_mul(sW[2], sW[3]));
-        const int64_t v = (t >> 1) == 0 ? tot.pp : (t >> 1) == 1 ? tot.pm : (t >> 1) == 2 ? tot.mp : tot.mm;
-        const uint32_t half = (t & 1) ? (uint32_t)((uint64_t)v >> 32) : (uint32_t)v;
-        __hip_atomic_store(as.agg + (int64_t)blockIdx.x * 8 + t,
-                           ((unsigned long long)as.epoch << 32) | half, __ATOMIC_RELAXED,
-                           __HIP_MEMORY_SCOPE_AGENT);
-    }
-    if (t < 8 * sidx) {
-        const unsigned long long* src = as.agg + ((int64_t)blockIdx.x - sidx + (t >> 3)) * 8 + (t & 7);
-        const unsigned long long t0 = wall_clock64();
-        unsigned long long f;
-        for (;;) {
-            // deadline first: a limit of 0 gives up deterministically (the test hook)
-            if (wall_clock64() - t0 >= (unsigned long long)(CPG_VIT_SPIN_LIMIT)) {
-                atomicOr(as.status, ST_VIT_LOOKBACK);
-                f = 0;
-                break;
-            }
-            f = __hip_atomic_load(src, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if ((uint32_t)(f >> 32) == as.epoch) break;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        sPre[t] = f;
-    }
-    __syncthreads();
-    if (t == 0) {   // the segment's entry estimate: the chunk's start times the earlier products
+    if (t == 0) {   // the segment's entry estimate
         const int f = vc.qshift;
         int64_t P = fix_of(lp, f), M = fix_of(lm, f);
-        for (int j = 0; j < sidx; ++j) {
-            const unsigned long long* w = sPre + 8 * j;
-            auto val = [&](int i) {
-                return (int64_t)(((uint64_t)(uint32_t)w[2 * i + 1] << 32) | (uint32_t)w[2 * i]);
-            };
-            ci_apply(P, M, CI{val(0), val(1), val(2), val(3)});
-        }
+        for (int j = 0; j < sidx; ++j) ci_apply(P, M, sPre[j]);
         sEnt = make_longlong2(P, M);
     }
     __syncthreads();
@@ -2119,9 +2099,10 @@ __device__ __forceinline__ void trace_tile(const uint32_t (&out)[8], const uint3
     if (t == 0) st_cnt5<kAgent>(tl.ttot + tile, tot);
 }
 
-// kIsl: 0 = the traceback alone; 1 = + the island tile of its workgroup + the chunk's resolve
-// in the chunk's last workgroup (fused decode, <= 256 chunks); 2 = + the island tile only, the
-// resolve kernels run after it (fused decode past 256 chunks: no re-read of bases and signs)
+// kIsl: 0 = the traceback alone; 1 = + the island tile of its workgroup + the chunk's first
+// resolve pass in the chunk's last workgroup (fused decode, <= 256 chunks; the records are
+// placed by the write pass after it); 2 = + the island tile only, both resolve kernels run
+// after it (fused decode past 256 chunks: no re-read of bases and signs)
 template <int kIsl>
 __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __restrict__ bp,
                                                         const uint8_t* __restrict__ endst,
@@ -2203,8 +2184,9 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
     if constexpr (kIsl == 2) trace_tile<false>(out, P, pprev, sb << 31, k, fz.ws, blockIdx.x);
     if constexpr (kIsl == 1) {
         trace_tile<true>(out, P, pprev, sb << 31, k, fz.ws, blockIdx.x);
-        // the chunk's last workgroup to finish resolves it (its records are complete): the
-        // island resolve kernel's work, overlapped with the other chunks' tracebacks
+        // the chunk's last workgroup to finish runs its first resolve pass (its run records are
+        // complete; a done counter, nothing waits): the resolve kernel's work, overlapped with
+        // the other chunks' tracebacks
         __shared__ int s_last;
         __builtin_amdgcn_s_waitcnt(0);   // this wave's record stores have completed
         __syncthreads();
@@ -2220,7 +2202,7 @@ __global__ __launch_bounds__(kThreads) void k_vit_trace(Geo g, const uint4* __re
         if (!s_last) return;
         __shared__ isl::ResolveLds L;
         __shared__ isl::Cnt5 s_to[kThreads / 16];
-        isl::resolve_chunk<true, kThreads / 16>(packed, g.C, fz.ws, fz.o, c, L, s_to);
+        isl::resolve_chunk<true, kThreads / 16>(packed, g.C, fz.ws, c, L, s_to);
     }
 }
 
@@ -2312,19 +2294,22 @@ hipError_t launch_viterbi(const VitConsts& vc, const VitTables* d_vt, const uint
     // (as K3's extra workgroups it cost K3 0.9 us more: measured, not kept)
     const unsigned head = (unsigned)((nchunks + kScanT - 1) / kScanT);
     // the segment path for chunks of whole 256-block segments, at most kMaxSeg of them (the
-    // reference's 1 Mi decode chunk: 16): K2 folded into K1 (segment scans + look-back), block
-    // 0's walk in K3's launch, K4 over barriers and segment summaries only; rx in the gk slot
+    // reference's 1 Mi decode chunk: 16): K1 also forms each segment's product, K2 runs per
+    // segment (k_vit_segplan), block 0's walk in K3's launch, K4 over barriers and segment
+    // summaries only; rx in the gk slot
     const bool segp = nsb % kThreads == 0 && nsb / kThreads <= kMaxSeg && chunk_len == nsb * kSB;
     SegSum* sg = segp ? w.seg : nullptr;
-    ApproxSeg as{nullptr, 0, w.aent, w.degen, w.plan, w.splitlist, w.irrseg, status};
-    if (segp) {   // the segment products in their own slot (WS_VAGG), a fresh tag per call
+    ApproxSeg as{nullptr, w.aent, w.degen, w.plan, w.splitlist, w.irrseg};
+    if (segp) {   // the segment products (WS_VAGG)
         if (!agg) return hipErrorInvalidValue;
-        as.agg = agg;
-        as.epoch = lookback_epoch();
+        as.segprod = reinterpret_cast<CI*>(agg);
     }
     hipLaunchKernelGGL(k_vit_approx, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, d_vt,
                        w.comp1, as);
-    if (!segp)
+    if (segp)
+        hipLaunchKernelGGL(k_vit_segplan, dim3(grid), dim3(kThreads), 0, s, vc, packed, g, w.comp1,
+                           as);
+    else
         hipLaunchKernelGGL(k_vit_scan, dim3((unsigned)nchunks + head), dim3(kScanT), 0, s, vc,
                            packed, g, w.comp1, w.aent, w.degen, w.plan, w.splitlist, w.splitcount,
                            w.vhead);

@@ -122,11 +122,10 @@ int         cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags);
 int         cpg_workspace_bytes(cpg_ctx* ctx, int64_t* bytes);
 /* Wait for `stream` and return the first kernel-reported status since the last
  * cpg_sync: CPG_OK; CPG_E_VERIFY (a Viterbi exactness self-check failed); CPG_E_INVALID
- * (a broken contig layout); CPG_E_DEVICE when a bounded look-back gave up — the island
- * kernel's (the island records and count of that call are unusable) or the Viterbi
- * segment look-back's (the decoded path and scores of that call are unusable).  The
- * outputs of cpg_viterbi_d / cpg_decode_d / cpg_islands_d are valid only once cpg_sync
- * has returned CPG_OK for them. */
+ * (a broken contig layout); CPG_E_UNSUPPORTED (a general-model path not representable as
+ * sign bits); CPG_E_DEVICE (the device reader, cpg_ingest_d).  No kernel of the decode /
+ * island entry points waits for another workgroup.  The outputs of cpg_viterbi_d /
+ * cpg_decode_d / cpg_islands_d are valid only once cpg_sync has returned CPG_OK for them. */
 int         cpg_sync(cpg_ctx* ctx, void* stream);
 /* A HIP stream whose kernels run only on the compute units set in cu_mask (mask_words
  * 32-bit words, bit i = compute unit i in the runtime's order): partitions the GPU between
@@ -223,8 +222,8 @@ int cpg_merge_train_d(cpg_ctx* ctx, const void* d_gathered, int world, double* d
  * whole chunk_len chunk (tail not decoded, :256).  Output: the state path as sign bits
  * (state = base + (sign ? 0 : 4)), identical to Mahout's sequential fp64 Viterbi, and
  * the final best log-probability per chunk (d_score, may be NULL).  Asynchronous: the
- * outputs are valid once cpg_sync has returned CPG_OK (the kernels' self-checks and the
- * segment look-back report through it).
+ * outputs are valid once cpg_sync has returned CPG_OK (the kernels' self-checks report
+ * through it).
  * Models: the exact parallel scan takes deterministic emission rows (b[i][i%4] == 1),
  * 0 < a[i][j] <= 1 and 0 <= pi[i] <= 1; other models with deterministic emission rows (zero
  * transitions, pi outside) run Mahout's 8-state loop (cpg_viterbi_states_d's path), and

@@ -440,77 +440,47 @@ def test_islands_long_overflow_island(gpu_ctx, torch_dev):
     assert np.array_equal(D.islands_to_numpy(out, cnt), co.islands(st, 0))
 
 
-def test_islands_lookback_timeout_is_an_error(gpu_ctx):
-    """Only the fused decode's island resolve (cpg_decode_d, <= 256 chunks of a 64 Ki
-    multiple: the chunk's last traceback workgroup) finds its first record by a look-back over
-    earlier chunks' kept counts, a bounded spin.  libcpg_isl_timeout.so is built with that
-    bound forced to 0 (CPG_ISL_SPIN_LIMIT=0), so every chunk after the first gives up: the
-    call must fail with CPG_E_DEVICE (status bit ST_LOOKBACK_TIMEOUT via cpg_sync) instead of
-    returning records at wrong offsets.  The separate island kernels (cpg_islands*, and the
-    decode past 256 chunks) place records by a second kernel over the per-chunk counts: no
-    workgroup waits for another, so the same library returns the oracle's records there."""
-    import ctypes as C
-    import os
+def test_decode_on_two_cus_equals_full_gpu(gpu_ctx):
+    """No kernel of cpg_decode_d waits for another workgroup: K1 stores its segments' products
+    and the next launch (k_vit_segplan) reads the chunk's earlier ones; a fused decode's chunk
+    resolve (its last traceback workgroup, a done counter) writes per-chunk counts and the
+    write pass places the records.  So the decode on a stream of TWO compute units — where a
+    workgroup spinning on another could hold the units that one needs — completes, and equals
+    the whole GPU's decode and the two single calls bitwise (8 chunks of 1 Mi: the segment
+    path, 16 segments per chunk, and the fused island resolve)."""
     import torch
-    from cpgisland_amd import HmmModel, _lib
+    from cpgisland_amd import HmmModel
     from cpgisland_amd import device as D
-    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libcpg_isl_timeout.so")
-    assert os.path.exists(path), "build it: make -C cpgisland_amd/csrc"
-    lib = C.CDLL(path)
-    lib.cpg_open.argtypes = [C.c_int, C.c_void_p]
-    lib.cpg_close.argtypes = [C.c_void_p]
-    lib.cpg_last_error.restype = C.c_char_p
-    lib.cpg_sync.argtypes = [C.c_void_p, C.c_void_p]
-    lib.cpg_islands.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
-                                C.c_void_p, C.c_int64, C.c_void_p]
-    lib.cpg_decode_d.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
-                                 C.c_int64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64,
-                                 C.c_void_p, C.c_void_p]
-    rng = np.random.default_rng(7)
-    CL, nch = 4096, 8
-    states = np.concatenate([np.resize(_rand_states(rng), CL) for _ in range(nch)])
-    packed = np.ascontiguousarray(pr.pack((states % 4).astype(np.uint8)).astype(np.uint32))
-    sign = np.ascontiguousarray(pr.pack_bits((states < 4).astype(np.uint8)).astype(np.uint32))
-    out = np.zeros(4096, co.ISLAND_DTYPE)
-    cnt = C.c_int64(0)
-    exp = np.concatenate([co.islands(states[c * CL:(c + 1) * CL], c) for c in range(nch)])
     dev = torch.device("cuda:0")
-    n2, c2l = 8 * 65536, 65536
-    p2, _ = D.synth_host(11, 0, n2)
-    m = np.ascontiguousarray(co.initial_model())
-    dp2 = D.to_device(np.concatenate([p2, np.zeros(8, np.uint32)]), dev)
-    so = torch.zeros(D.words32(n2) + 4, dtype=torch.int32, device=dev)
-    sc = torch.zeros(8, dtype=torch.float64, device=dev)
-    io = torch.zeros((4096, 32), dtype=torch.uint8, device=dev)
-    ic = torch.zeros(1, dtype=torch.int64, device=dev)
-    ctx = C.c_void_p()
-    assert lib.cpg_open(0, C.byref(ctx)) == 0
+    n, cl = 8 << 20, 1 << 20
+    p, _ = D.synth_host(11, 0, n)
+    dp = D.to_device(np.concatenate([p, np.zeros(8, np.uint32)]), dev)
+    m = HmmModel.initial()
+    so, sc, io, ic = D.decode(gpu_ctx, m, dp, n, cl)
+    s2 = D.cu_stream(0, [0, 1])
     try:
-        rc = lib.cpg_islands(ctx, packed.ctypes.data, sign.ctypes.data, nch * CL, CL,
-                             out.ctypes.data, len(out), C.byref(cnt))
-        assert rc == 0, lib.cpg_last_error()
-        assert np.array_equal(out[:cnt.value], exp)
-        torch.cuda.synchronize()
-        rc = lib.cpg_decode_d(ctx, m.ctypes.data, dp2.data_ptr(), n2, c2l, 0, so.data_ptr(),
-                              sc.data_ptr(), io.data_ptr(), 4096, ic.data_ptr(), None)
-        assert rc == 0
-        rc = lib.cpg_sync(ctx, None)
-        assert rc == _lib.CPG_E_DEVICE, rc
-        assert b"look-back" in lib.cpg_last_error()
-        # the status word was consumed: the same context works again
-        rc1 = lib.cpg_islands(ctx, packed.ctypes.data, sign.ctypes.data, CL, CL,
-                              out.ctypes.data, len(out), C.byref(cnt))
-        assert rc1 == 0
-        assert np.array_equal(out[:cnt.value], co.islands(states[:CL], 0))
+        with torch.cuda.stream(s2):
+            so2, sc2, io2, ic2 = D.decode(gpu_ctx, m, dp, n, cl)
+        s2.synchronize()
     finally:
-        lib.cpg_close(ctx)
-    # the product library: the fused decode's records equal the separate calls' (no timeout)
-    so2, sc2, io2, ic2 = D.decode(gpu_ctx, HmmModel.initial(), dp2, n2, c2l)
-    so3, _ = D.viterbi(gpu_ctx, HmmModel.initial(), dp2, n2, c2l)
-    o3, c3 = D.islands(gpu_ctx, dp2, so3, n2, c2l)
+        D.cu_stream_destroy(s2)
+    so3, sc3 = D.viterbi(gpu_ctx, m, dp, n, cl)
+    o3, c3 = D.islands(gpu_ctx, dp, so3, n, cl)
     torch.cuda.synchronize()
     gpu_ctx.sync()
-    assert np.array_equal(D.islands_to_numpy(io2, ic2), D.islands_to_numpy(o3, c3))
+    w = D.words32(n)
+    for a_, b_ in ((so2, so), (so3, so)):
+        assert np.array_equal(a_.cpu().numpy()[:w], b_.cpu().numpy()[:w])
+    assert np.array_equal(sc2.cpu().numpy(), sc.cpu().numpy())
+    assert np.array_equal(sc3.cpu().numpy(), sc.cpu().numpy())
+    isl = D.islands_to_numpy(io, ic)
+    assert len(isl) > 0
+    assert np.array_equal(D.islands_to_numpy(io2, ic2), isl)
+    assert np.array_equal(D.islands_to_numpy(o3, c3), isl)
+    st, best = co.viterbi8(m.to_struct(), pr.unpack(p[: cl // 16], cl))
+    assert np.array_equal(D.sign_to_numpy(so, cl), (st < 4).astype(np.uint8))
+    assert sc.cpu().numpy()[0] == best
+    assert np.array_equal(isl[isl["chunk"] == 0], co.islands(st, 0))
 
 
 def test_islands_capacity(gpu_ctx, torch_dev, golden):
@@ -783,42 +753,3 @@ def test_merge_train_records(gpu_ctx, torch_dev, world):
     rc.copy_(torch.from_numpy(c[0]))
     cd.merge_train_records(gpu_ctx, rec, oe, oc)
     assert np.array_equal(oe.cpu().numpy(), e[0]) and np.array_equal(oc.cpu().numpy(), c[0])
-
-
-def test_viterbi_lookback_timeout_is_an_error(gpu_ctx):
-    """The Viterbi segment path's look-back over a chunk's earlier segments (K1) is a bounded
-    spin; in libcpg_isl_timeout.so the bound is 0 (CPG_VIT_SPIN_LIMIT=0), so every segment
-    after a chunk's first gives up: the call fails with CPG_E_DEVICE (ST_VIT_LOOKBACK) instead
-    of returning a path.  Chunks of one segment (64 Ki) have no look-back and still decode."""
-    import ctypes as C
-    import os
-    from cpgisland_amd import _lib
-    path = os.path.join(os.path.dirname(_lib.LIB_PATH), "libcpg_isl_timeout.so")
-    assert os.path.exists(path), "build it: make -C cpgisland_amd/csrc"
-    lib = C.CDLL(path)
-    lib.cpg_open.argtypes = [C.c_int, C.c_void_p]
-    lib.cpg_close.argtypes = [C.c_void_p]
-    lib.cpg_last_error.restype = C.c_char_p
-    lib.cpg_viterbi.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_int64, C.c_int64,
-                                C.c_void_p, C.c_void_p]
-    n = 2 << 20
-    packed, _ = __import__("cpgisland_amd.device", fromlist=["synth_host"]).synth_host(5, 0, n)
-    packed = np.ascontiguousarray(packed.astype(np.uint32))
-    m = np.ascontiguousarray(co.initial_model())
-    sign = np.zeros(n // 32 + 4, np.uint32)
-    score = np.zeros(64, np.float64)
-    ctx = C.c_void_p()
-    assert lib.cpg_open(0, C.byref(ctx)) == 0
-    try:
-        rc = lib.cpg_viterbi(ctx, m.ctypes.data, packed.ctypes.data, n, 1 << 20,
-                             sign.ctypes.data, score.ctypes.data)
-        assert rc == _lib.CPG_E_DEVICE, rc
-        assert b"look-back" in lib.cpg_last_error()
-        rc1 = lib.cpg_viterbi(ctx, m.ctypes.data, packed.ctypes.data, n, 65536,
-                              sign.ctypes.data, score.ctypes.data)
-        assert rc1 == 0
-        st, best = co.viterbi8(m, pr.unpack(packed, 65536))
-        assert np.array_equal(pr.unpack_bits(sign, 65536), (st < 4).astype(np.uint8))
-        assert score[0] == best
-    finally:
-        lib.cpg_close(ctx)

@@ -31,5 +31,4 @@ make -s -j8 -C $SRC/csrc OBJDIR=$ROOT/build/abl/obj_$NAME OUT=$ROOT/build/abl/li
 P=$ROOT/build/abl/pkg_$NAME/cpgisland_amd
 rm -rf $P && mkdir -p $P
 cp $ROOT/cpgisland_amd/*.py $P/ && cp $ROOT/build/abl/libcpg_$NAME.so $P/libcpg.so
-[ -f $ROOT/cpgisland_amd/libcpg_isl_timeout.so ] && cp $ROOT/cpgisland_amd/libcpg_isl_timeout.so $P/
 echo "built $ROOT/build/abl/libcpg_$NAME.so"
