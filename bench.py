@@ -542,7 +542,7 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
     tr_o, tr_n = pl.t0 * TRAIN - pl.base, (pl.t1 - pl.t0) * TRAIN
     de_o, de_n = pl.d0 * DECODE - pl.base, (pl.d1 - pl.d0) * DECODE
     ctx = Context(local)
-    ctx.reserve(max(span, 1))
+    ctx.reserve(max(span, 1), chunk_len=DECODE)
     model0 = HmmModel.initial()
     icap = de_n // 32768 + 2048   # island records per rank per step (~3x the ~1 per 100 kbp)
     nd_total = G // DECODE
@@ -937,7 +937,7 @@ def main():
     dp = D.to_device(packed, dev)
     ds = D.to_device(sign, dev)
     ctx = Context(local)
-    ctx.reserve(N)
+    ctx.reserve(N, chunk_len=DECODE)
     model0 = HmmModel.initial()
     ndec = N // DECODE
     first_chunk = start // DECODE

@@ -59,6 +59,7 @@ SIGNATURES = {
     "cpg_abi_version": [],
     "cpg_reserve": [_P, _I64],
     "cpg_reserve_ex": [_P, _I64, _INT],
+    "cpg_reserve_chunk": [_P, _I64, _I64, _INT],
     "cpg_workspace_bytes": [_P, _P],
     "cpg_sync": [_P, _P],
     "cpg_stream_create_cu": [_INT, _P, _INT, _P],

@@ -29,6 +29,17 @@ __device__ __forceinline__ uint32_t bfi(uint32_t m, uint32_t x, uint32_t y) {
     return (m & x) | (~m & y);
 #endif
 }
+// c + popcount(x) as ONE v_bcnt_u32_b32 (its second operand is the addend): the compiler pairs
+// two popcounts with a v_add3 instead, three instructions where two do
+__device__ __forceinline__ uint32_t bcnt_acc(uint32_t x, uint32_t c) {
+#if defined(__gfx950__)
+    uint32_t r;
+    asm("v_bcnt_u32_b32 %0, %1, %2" : "=v"(r) : "v"(x), "v"(c));
+    return r;
+#else
+    return c + __popc(x);
+#endif
+}
 // 16 bits (bit k) -> even bit positions (bit 2k)
 __device__ __forceinline__ uint32_t spread16(uint32_t x) {
     x &= 0xFFFFu;
@@ -77,11 +88,11 @@ struct Lane {
     // the sign bit before the block (ignored at a chunk start: no transition into position 0);
     // valid = false: a lane without a block (counts nothing).  EVERY lane of the wave calls
     // (the '+' work below reduces over the wave).
-    __device__ __forceinline__ void block(uint4 w, uint2 s, uint32_t wprev, uint32_t sprev,
-                                          bool cstart, uint32_t* lds, bool valid = true) {
-        if (cstart) sprev = 0u;
-        const uint32_t vm = valid ? ~0u : 0u;
-        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+    // the 15 all-transition moments of the block's 64 positions into c[1..15]; kMask: pair 0's
+    // planes masked by pm0 (a chunk start: no transition into position 0), pair 1's by vm
+    template <bool kMask>
+    __device__ __forceinline__ void moments(const uint32_t (&ww)[4], uint32_t wprev, uint32_t pm0,
+                                            uint32_t vm) {
         uint32_t last = wprev;
 #pragma unroll
         for (int pr = 0; pr < 2; ++pr) {
@@ -94,16 +105,30 @@ struct Lane {
             // a[15] (bit 30 of the planes) — through bits 30 / 31 of an aligned pair
             uint32_t PLO = __builtin_amdgcn_alignbit(LO, bfi(0x80000000u, LO << 1, last), 30);
             uint32_t PHI = __builtin_amdgcn_alignbit(HI, bfi(0x80000000u, HI << 1, last >> 1), 30);
-            // no transition into a chunk's position 0, nothing from a lane without a block
-            const uint32_t pm = (pr == 0 && cstart) ? (vm & ~1u) : vm;
-            LO &= pm; HI &= pm; PLO &= pm; PHI &= pm;
+            if constexpr (kMask) {
+                const uint32_t pm = pr == 0 ? pm0 : vm;
+                LO &= pm; HI &= pm; PLO &= pm; PHI &= pm;
+            }
             last = b;
             const uint32_t lh = LO & HI, pq = PLO & PHI;
             const uint32_t x[16] = {0u, LO, HI, lh, PLO, LO & PLO, HI & PLO, lh & PLO,
                                     PHI, LO & PHI, HI & PHI, lh & PHI, pq, LO & pq, HI & pq, lh & pq};
 #pragma unroll
-            for (int j = 1; j < 16; ++j) c[j] += __popc(x[j]);
+            for (int j = 1; j < 16; ++j) c[j] = bcnt_acc(x[j], c[j]);
         }
+    }
+    __device__ __forceinline__ void block(uint4 w, uint2 s, uint32_t wprev, uint32_t sprev,
+                                          bool cstart, uint32_t* lds, bool valid = true) {
+        if (cstart) sprev = 0u;
+        const uint32_t vm = valid ? ~0u : 0u;
+        const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
+        // no transition into a chunk's position 0, nothing from a lane without a block: the
+        // masks only in a wave with such a lane (a wave-uniform branch; chunk starts are 1 in
+        // 1,024 blocks at the reference's chunk length)
+        if (__builtin_amdgcn_ballot_w64(cstart || !valid))
+            moments<true>(ww, wprev, cstart ? (vm & ~1u) : vm, vm);
+        else
+            moments<false>(ww, wprev, ~0u, ~0u);
         c[0] += valid ? (cstart ? 63u : 64u) : 0u;
         // the '+' work (rare: island blocks)
         const bool plus = valid && (s.x | s.y | sprev) != 0u;

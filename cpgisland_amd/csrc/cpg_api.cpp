@@ -221,25 +221,20 @@ void cpg_close(cpg_ctx* ctx) {
 
 int cpg_reserve(cpg_ctx* ctx, int64_t nbases) { return cpg_reserve_ex(ctx, nbases, 0); }
 
-int cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags) {
-    if (!ctx || nbases < 0 || (flags & ~CPG_RESERVE_GENERAL))
-        return set_error(CPG_E_INVALID, "bad argument");
-    std::lock_guard<std::mutex> lk(ctx->mu);
-    CPG_HIP(hipSetDevice(ctx->device));
+// the workspace every entry point needs for inputs of up to nbases bases, at the decode chunk
+// lengths C in [c_lo, c_hi] stepping c_step (host arithmetic only)
+static int reserve_lengths(cpg_ctx* ctx, int64_t nbases, int flags, int64_t c_lo, int64_t c_hi,
+                           int64_t c_step) {
     void* p;
     int rc;
-    // every slot at its largest over ALL the chunk lengths the decode entry points take
-    // (every multiple of 256 up to the reference's 1 Mi — a non-power-of-two length takes
-    // another carve): the per-chunk slots (look-back words, done counters) grow with the chunk
-    // count, so a reserve for 1 Mi chunks alone would still let a later call with shorter
-    // chunks grow a slot — a device-wide synchronisation (ws_get).  Host arithmetic only
-    // (4,096 lengths).
     size_t vit = 0, isl = 0, agg = 0, per_chunk = 0;
-    for (int64_t C = 256; C <= CPG_DECODE_CHUNK; C += 256) {
+    for (int64_t C = c_lo; C <= c_hi; C += c_step) {
         const int64_t nd = nbases / C + 1;
-        vit = std::max(vit, viterbi_ws_bytes(nd, C));
+        // (the Viterbi: several chunks of a multiple of 256, or one chunk of any length)
+        const int64_t ndv = C % 256 == 0 ? nd : 1;
+        vit = std::max(vit, viterbi_ws_bytes(ndv, C));
+        agg = std::max(agg, viterbi_agg_bytes(ndv, C));
         isl = std::max(isl, islands_ws_bytes(nd, C));
-        agg = std::max(agg, viterbi_agg_bytes(nd, C));
         per_chunk = std::max(per_chunk, (size_t)(nd + 1) * 8);
     }
     const int64_t nt = nbases / 256 + 1;
@@ -259,6 +254,27 @@ int cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags) {
         if ((rc = ws_get(ctx, WS_VGEN, gen, &p))) return rc;
     }
     return CPG_OK;
+}
+
+int cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags) {
+    if (!ctx || nbases < 0 || (flags & ~CPG_RESERVE_GENERAL))
+        return set_error(CPG_E_INVALID, "bad argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    // every slot at its largest over ALL the chunk lengths the decode entry points take in
+    // whole 256-base blocks (every multiple of 256 up to the reference's 1 Mi — a
+    // non-power-of-two length takes another carve): the per-chunk slots grow with the chunk
+    // count, so a reserve for 1 Mi chunks alone would still let a later call with shorter
+    // chunks grow a slot (a device-wide synchronisation, ws_get)
+    return reserve_lengths(ctx, nbases, flags, 256, CPG_DECODE_CHUNK, 256);
+}
+
+int cpg_reserve_chunk(cpg_ctx* ctx, int64_t nbases, int64_t chunk_len, int flags) {
+    if (!ctx || nbases < 0 || chunk_len <= 0 || chunk_len % 32 || (flags & ~CPG_RESERVE_GENERAL))
+        return set_error(CPG_E_INVALID, "bad argument");
+    std::lock_guard<std::mutex> lk(ctx->mu);
+    CPG_HIP(hipSetDevice(ctx->device));
+    return reserve_lengths(ctx, nbases, flags, chunk_len, chunk_len, 1);
 }
 
 int cpg_workspace_bytes(cpg_ctx* ctx, int64_t* bytes) {

@@ -3,7 +3,7 @@
 // Training-side counterpart of the BW mapper stripes (init / transition / emission rows,
 // CpGIslandFinder.java:200) computed from hard labels: state s_t = base_t + (sign_t?0:4).
 // Streams 2-bit packed bases (16 B per lane = 64 bases) and sign bits (8 B per lane) in
-// grid-stride batches, the next batch's loads in flight while a batch is counted, and counts
+// grid-stride rounds, the next round's loads in flight while a round is counted, and counts
 // with v_bcnt over the bases' bit-planes (count_dev.h; shared with the fused training pass in
 // k_estep.hip).
 //
@@ -24,10 +24,8 @@ namespace {
 using cnt::kRaw;
 constexpr int kCountThreads = 256;
 constexpr int kCntRep = cnt::kRep;
-// blocks per lane per batch, and the grid cap: 4 waves per SIMD (<= 128 VGPRs) hold 1,024
-// workgroups of 4 waves at once; every lane has two batches in flight (the one being counted
-// and the next one's loads)
-constexpr int kBatch = 1;
+// the grid cap: 4 waves per SIMD (<= 128 VGPRs) hold 1,024 workgroups of 4 waves at once;
+// every lane has two rounds in flight (the one being counted and the next one's loads)
 constexpr int kCntGrid = 2048;
 constexpr int kCntWavesPerEU = 4;
 
@@ -36,40 +34,29 @@ __device__ __forceinline__ uint32_t from_lane_below(uint32_t v, uint32_t old) {
     return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)v, 0x138, 0xF, 0xF, false);
 }
 
-// One batch of a wave: block g + lane + r * stride of each lane, r < kBatch (the wave's 64
-// lanes read 64 consecutive blocks: coalesced 16-B and 8-B loads off a wave-uniform base with
-// 32-bit lane offsets), plus the packed word and sign word before the wave's first block of
-// each round (wave-uniform addresses); the other lanes' words before their block are the lane
-// below's last words (DPP, no load).  Offsets clamped to the last block: no branch around a
-// load.
-struct Batch {
-    uint4 w[kBatch];
-    uint2 s[kBatch];
-    uint32_t wp0[kBatch], sp0[kBatch];
+// One wave-round: the 64 consecutive blocks g .. g+63, block g + lane in lane `lane` (coalesced
+// 16-B packed and 8-B label loads off a wave-uniform base), plus the packed word and the label
+// word before block g (wave-uniform addresses); the other lanes' words before their block are
+// the lane below's last words (DPP, no load).
+struct Round {
+    uint4 w;
+    uint2 s;
+    uint32_t wp0, sp0;
 };
-__device__ __forceinline__ void load_batch(Batch& b, const uint4* __restrict__ packed4,
+// a full round (every block < nblk): no clamp, no validity.  zv: an opaque zero in a VGPR, so
+// that the wave-uniform loads stay VECTOR loads, counted in order with the round's other loads
+// (as scalar loads they made every round wait lgkmcnt(0) — for the NEXT round's scalar loads
+// too, which SMEM returns out of order)
+__device__ __forceinline__ void load_round(Round& r, const uint4* __restrict__ packed4,
                                            const uint2* __restrict__ sign2,
                                            const uint32_t* __restrict__ packed,
-                                           const uint32_t* __restrict__ sign, int64_t g,
-                                           int lane, uint32_t stride, int64_t nblk, uint32_t zv) {
-    const int64_t lim64 = nblk - 1 - g;   // wave-uniform; >= 0 for the rounds that count
-    const uint32_t lim = lim64 < 0 ? 0u : lim64 > 0x7FFFFFFF ? 0x7FFFFFFFu : (uint32_t)lim64;
-    const uint4* pb = packed4 + min(g, nblk - 1);
-    const uint2* sb = sign2 + min(g, nblk - 1);
-    const uint32_t base_ok = g < nblk ? 1u : 0u;   // (past the end: every offset 0)
-#pragma unroll
-    for (int r = 0; r < kBatch; ++r) {
-        const uint32_t o = min((uint32_t)lane + (uint32_t)r * stride, lim) * base_ok;
-        b.w[r] = pb[o];
-        b.s[r] = sb[o];
-        // (zv: an opaque zero in a VGPR, so that these wave-uniform loads stay VECTOR loads,
-        // counted in order with the batch's other loads: as scalar loads they made every
-        // batch wait lgkmcnt(0) — for the NEXT batch's scalar loads too, which SMEM returns
-        // out of order)
-        const int64_t ip = min(max(g + (int64_t)r * stride - 1, (int64_t)0), nblk - 1);
-        b.wp0[r] = packed[4 * ip + 3 + zv];
-        b.sp0[r] = sign[2 * ip + 1 + zv];
-    }
+                                           const uint32_t* __restrict__ sign, int64_t g, int lane,
+                                           uint32_t zv) {
+    r.w = (packed4 + g)[lane];
+    r.s = (sign2 + g)[lane];
+    const int64_t ip = g > 0 ? g - 1 : 0;   // (block 0 is a chunk start: its word is unused)
+    r.wp0 = packed[4 * ip + 3 + zv];
+    r.sp0 = sign[2 * ip + 1 + zv];
 }
 
 // done != nullptr: the last workgroup to finish also finalizes (one launch per call).
@@ -89,49 +76,50 @@ void k_count_main(const uint4* __restrict__ packed4, const uint2* __restrict__ s
     spp[t] = 0u;   // (kCountThreads == 256 == 16 x 16)
     __syncthreads();
     cnt::Lane lc(spp);
-    const uint32_t stride = gridDim.x * blockDim.x;
-    const int64_t step = (int64_t)kBatch * stride;
-    // the wave's first block (wave-uniform): every lane of a wave runs every batch, so the
+    const int64_t step = (int64_t)gridDim.x * blockDim.x;   // blocks per grid round
+    // the wave's first block (wave-uniform): every lane of a wave runs every round, so the
     // flush's shuffles see the whole wave
     int64_t g = (int64_t)blockIdx.x * blockDim.x + __builtin_amdgcn_readfirstlane(t & ~63);
-    // kTail: the last round, some of whose blocks lie past the end (their lanes count
-    // nothing; the full rounds carry no validity test)
-    auto count = [&](const Batch& b, int64_t gb, auto tail) {
-        constexpr bool kTail = decltype(tail)::value;
-#pragma unroll
-        for (int r = 0; r < kBatch; ++r) {
-            const uint32_t o = (uint32_t)lane + (uint32_t)r * stride;
-            const uint32_t wp = from_lane_below(b.w[r].w, b.wp0[r]);
-            const uint32_t sp = from_lane_below(b.s[r].y, b.sp0[r]) >> 31;
-            const bool valid = !kTail || gb + (int64_t)o < nblk;
-            // (a power-of-two chunk — the reference's 0x10000 — needs no 64-bit modulo)
-            const bool cstart = kPow2 ? (((uint32_t)gb + o) & (uint32_t)(blk_per_chunk - 1)) == 0u
-                                      : ((gb + (int64_t)o) % blk_per_chunk) == 0;
-            if (valid && cstart) atomicAdd(&scnt[64 + cnt::init_state(b.w[r].x, b.s[r].x)], 1u);
-            lc.block(b.w[r], b.s[r], wp, sp, cstart, scnt, valid);   // (every lane calls)
-        }
+    auto chunk_start = [&](int64_t b) {
+        // (a power-of-two chunk — the reference's 0x10000 — needs no 64-bit modulo)
+        return kPow2 ? ((uint32_t)b & (uint32_t)(blk_per_chunk - 1)) == 0u : (b % blk_per_chunk) == 0;
     };
-    // two batches in flight per lane: the next batch's loads are issued before the current
-    // one is counted (ping-pong buffers)
-    // a round is full when the wave's last block of it lies before the end (wave-uniform)
-    const int64_t span = (int64_t)(kBatch - 1) * stride + 63;
-    auto count_round = [&](const Batch& b, int64_t gb) {
-        if (gb + span < nblk) count(b, gb, std::false_type{});
-        else count(b, gb, std::true_type{});
+    auto count_round = [&](const Round& r, int64_t gb, bool valid) {
+        const uint32_t wp = from_lane_below(r.w.w, r.wp0);
+        const uint32_t sp = from_lane_below(r.s.y, r.sp0) >> 31;
+        const bool cstart = valid && chunk_start(gb + lane);
+        if (cstart) atomicAdd(&scnt[64 + cnt::init_state(r.w.x, r.s.x)], 1u);
+        lc.block(r.w, r.s, wp, sp, cstart, scnt, valid);   // (every lane calls)
     };
     uint32_t zv;
     asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
-    Batch A, B;
-    load_batch(A, packed4, sign2, packed, sign, g, lane, stride, nblk, zv);
-    while (g < nblk) {
-        load_batch(B, packed4, sign2, packed, sign, g + step, lane, stride, nblk, zv);
-        count_round(A, g);
+    // full rounds, two per iteration: the next round's loads are issued before the current one
+    // is counted (ping-pong buffers); a round is full when the wave's last block of it lies
+    // before the end (wave-uniform)
+    const int64_t gfull = nblk - 64;
+    Round A, B;
+    if (g <= gfull) load_round(A, packed4, sign2, packed, sign, g, lane, zv);
+    while (g <= gfull) {
+        if (g + step <= gfull) load_round(B, packed4, sign2, packed, sign, g + step, lane, zv);
+        count_round(A, g, true);
         g += step;
-        if (g < nblk) {
-            load_batch(A, packed4, sign2, packed, sign, g + step, lane, stride, nblk, zv);
-            count_round(B, g);
-            g += step;
-        }
+        if (g > gfull) break;
+        if (g + step <= gfull) load_round(A, packed4, sign2, packed, sign, g + step, lane, zv);
+        count_round(B, g, true);
+        g += step;
+    }
+    // the grid's last, partial round (at most one wave has it): lanes past the end count
+    // nothing (every lane still calls: the wave reductions)
+    if (g < nblk) {
+        const bool valid = g + lane < nblk;
+        const int64_t bb = valid ? g + lane : nblk - 1;
+        Round r;
+        r.w = packed4[bb];
+        r.s = sign2[bb];
+        const int64_t ip = g > 0 ? g - 1 : 0;
+        r.wp0 = packed[4 * ip + 3 + zv];
+        r.sp0 = sign[2 * ip + 1 + zv];
+        count_round(r, g, valid);
     }
     lc.flush(scnt);   // (32-bit counters: a lane's blocks are far below their range)
     __syncthreads();
@@ -167,9 +155,9 @@ hipError_t launch_count(const uint32_t* packed, const uint32_t* sign, int64_t nc
     const int64_t nblk = nchunks * chunk_len / 64;
     if (nblk <= 0 && parts == PART_ALL) return hipMemsetAsync(out, 0, 124 * sizeof(int64_t), s);
     if ((parts & PART_ACC) && nblk > 0) {
-        // at most one batch per lane when the input is small (46 Mbp: ~0.7 batches per lane
+        // at most one round per lane when the input is small (46 Mbp: ~0.7 rounds per lane
         // of 1,024 workgroups), the grid cap when it is large
-        int64_t grid = (nblk + (int64_t)kCountThreads * kBatch - 1) / ((int64_t)kCountThreads * kBatch);
+        int64_t grid = (nblk + (int64_t)kCountThreads - 1) / kCountThreads;
         if (grid > kCntGrid) grid = kCntGrid;
         // the whole call in one launch: its last workgroup finalizes
         unsigned int* done = parts == PART_ALL ? (unsigned int*)(ws + kRaw * kCntRep) : nullptr;

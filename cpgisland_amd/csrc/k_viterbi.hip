@@ -1688,6 +1688,9 @@ __device__ __forceinline__ uint32_t push_bit(uint32_t w, bool c) {
 // nibble shifted into a byte whose other bits are dropped, a high nibble masked in place
 // (the shift + mask pair they replace was two ops per step of K5's walk)
 __device__ __forceinline__ uint32_t nib16(uint32_t w, int m) {
+#if !defined(__gfx950__)   // (SDWA is a gfx9-family encoding: other targets shift + mask)
+    return ((w >> (4 * m)) & 15u) << 4;
+#else
     uint32_t r;
     const uint32_t f0 = 0xF0u;
     switch (m) {
@@ -1701,6 +1704,7 @@ __device__ __forceinline__ uint32_t nib16(uint32_t w, int m) {
         default: asm("v_and_b32_sdwa %0, %1, %2 dst_sel:DWORD dst_unused:UNUSED_PAD src0_sel:DWORD src1_sel:BYTE_3" : "=v"(r) : "v"(f0), "v"(w)); break;
     }
     return r;
+#endif
 }
 
 // origin map (bit x = origin sign of the state-x survivor, '+' = 1) of 64 steps from their

@@ -95,10 +95,16 @@ class Context:
     def sync(self, stream=None):
         check(lib.cpg_sync(self.handle, stream))
 
-    def reserve(self, nbases: int, general: bool = False):
-        """cpg_reserve / cpg_reserve_ex: size the workspace for inputs of up to nbases bases
-        (general=True: also the general-model Viterbi's, ~26 B per base)."""
-        check(lib.cpg_reserve_ex(self.handle, int(nbases), 1 if general else 0))
+    def reserve(self, nbases: int, general: bool = False, chunk_len: int | None = None):
+        """cpg_reserve_ex: size the workspace for inputs of up to nbases bases at every decode
+        chunk length that is a multiple of 256 (general=True: also the general-model
+        Viterbi's, ~26 B per base); with chunk_len, cpg_reserve_chunk: for that one decode
+        chunk length only."""
+        if chunk_len is None:
+            check(lib.cpg_reserve_ex(self.handle, int(nbases), 1 if general else 0))
+        else:
+            check(lib.cpg_reserve_chunk(self.handle, int(nbases), int(chunk_len),
+                                        1 if general else 0))
 
     def workspace_bytes(self) -> int:
         """cpg_workspace_bytes: device workspace held by the context."""

@@ -105,11 +105,15 @@ int         cpg_open(int device, cpg_ctx** out);
 void        cpg_close(cpg_ctx* ctx);
 const char* cpg_last_error(void);
 int         cpg_abi_version(void);
-/* Pre-size the context's workspace for inputs of up to nbases bases, for every chunk length
- * the exact-scan entry points take (every multiple of 256 up to 1 Mi), so that the _d entry
- * points never allocate (required before hipGraph capture).  A slot that has to grow later (a
- * larger input) synchronises the whole device first: the old buffer may still be read by a
- * kernel on another stream.
+/* Pre-size the context's workspace for inputs of up to nbases bases, for every decode chunk
+ * length that is a multiple of 256 up to 1 Mi (the per-chunk slots at their largest: 256-base
+ * chunks), so that the _d entry points never allocate for those lengths (required before
+ * hipGraph capture).  Shorter island chunk lengths (cpg_islands_d / cpg_islands_at_d take
+ * any multiple of 32) and lengths past 1 Mi are outside this promise: such a call may grow a
+ * slot.  A slot that has to grow (a larger input, another chunk length) synchronises the
+ * whole device first: the old buffer may still be read by a kernel on another stream.
+ * cpg_reserve_chunk sizes for ONE decode chunk length instead (a caller on the reference's
+ * 1 Mi chunks does not pay for 256-base ones).
  * The general-model Viterbi (cpg_viterbi_states_d, and cpg_viterbi_d / cpg_decode_d /
  * cpg_decode_states for models outside the exact scan's contract) needs up to ~26 B of
  * workspace per base (its backpointer ballots); cpg_reserve does NOT size it: that path
@@ -118,6 +122,11 @@ int         cpg_abi_version(void);
 int         cpg_reserve(cpg_ctx* ctx, int64_t nbases);
 #define CPG_RESERVE_GENERAL 1   /* also size the general-model Viterbi's workspace */
 int         cpg_reserve_ex(cpg_ctx* ctx, int64_t nbases, int flags);
+/* As cpg_reserve_ex, for decode / island calls with this one chunk_len (a multiple of 32;
+ * > 1 chunk per call needs a multiple of 256 for the Viterbi) and the training chunk
+ * CPG_TRAIN_CHUNK; the _d entry points then never allocate for calls of at most nbases bases
+ * with that chunk length. */
+int         cpg_reserve_chunk(cpg_ctx* ctx, int64_t nbases, int64_t chunk_len, int flags);
 /* Device workspace currently held by the context, in bytes (all slots). */
 int         cpg_workspace_bytes(cpg_ctx* ctx, int64_t* bytes);
 /* Wait for `stream` and return the first kernel-reported status since the last

@@ -59,3 +59,39 @@ def test_workspace_growth_while_another_stream_reads():
         assert np.array_equal(D.sign_to_numpy(so2, n2)[:n1], want_sign)
     finally:
         ctx.close()
+
+
+def test_reserve_chunk_covers_its_chunk_length():
+    """ cpg_reserve_chunk sizes the workspace for ONE decode chunk length: after
+    it, the training pass, the fused decode and the island call at that length over up to
+    nbases bases allocate nothing (the context's workspace does not grow), and the reservation
+    is smaller than cpg_reserve's, which covers every multiple of 256."""
+    import torch
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    from cpgisland_amd import Context, HmmModel
+    from cpgisland_amd import device as D
+    dev = torch.device("cuda:0")
+    n = 43 * DECODE
+    p, s = D.synth_host(20251016, 0, n)
+    dp, ds = D.to_device(p, dev), D.to_device(s, dev)
+    a, b = Context(0), Context(0)
+    try:
+        a.reserve(n, chunk_len=DECODE)
+        b.reserve(n)
+        wa = a.workspace_bytes()
+        assert wa < b.workspace_bytes()
+        m = HmmModel.initial()
+        D.train_pass(a, m, dp, ds, n)
+        so, sc, io, ic = D.decode(a, m, dp, n, DECODE)
+        D.islands(a, dp, so, n, DECODE)
+        torch.cuda.synchronize()
+        a.sync()
+        assert a.workspace_bytes() == wa
+        so2, sc2, io2, ic2 = D.decode(b, m, dp, n, DECODE)
+        torch.cuda.synchronize()
+        b.sync()
+        assert np.array_equal(D.islands_to_numpy(io, ic), D.islands_to_numpy(io2, ic2))
+    finally:
+        a.close()
+        b.close()

@@ -13,6 +13,14 @@ import bench  # noqa: E402  (puts ROOT first on sys.path; imports no package mod
 if os.environ.get("CPG_DEV_PKG"):
     sys.path.insert(0, os.path.abspath(os.environ["CPG_DEV_PKG"]))
 assert "cpgisland_amd" not in sys.modules
+import inspect  # noqa: E402
+
+from cpgisland_amd import hmm as _hmm  # noqa: E402  (the variant's)
+
+if "chunk_len" not in inspect.signature(_hmm.Context.reserve).parameters:
+    # an older revision's Context: reserve() sizes for every chunk length anyway
+    _reserve = _hmm.Context.reserve
+    _hmm.Context.reserve = lambda self, n, general=False, chunk_len=None: _reserve(self, n, general)
 
 if __name__ == "__main__":
     bench.main()
