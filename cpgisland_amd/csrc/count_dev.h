@@ -90,7 +90,7 @@ struct Lane {
     // (the '+' work below reduces over the wave).
     // the 15 all-transition moments of the block's 64 positions into c[1..15]; kMask: pair 0's
     // planes masked by pm0 (a chunk start: no transition into position 0), pair 1's by vm
-    template <bool kMask>
+    template <bool kMask, bool kAsm>
     __device__ __forceinline__ void moments(const uint32_t (&ww)[4], uint32_t wprev, uint32_t pm0,
                                             uint32_t vm) {
         uint32_t last = wprev;
@@ -114,21 +114,25 @@ struct Lane {
             const uint32_t x[16] = {0u, LO, HI, lh, PLO, LO & PLO, HI & PLO, lh & PLO,
                                     PHI, LO & PHI, HI & PHI, lh & PHI, pq, LO & pq, HI & pq, lh & pq};
 #pragma unroll
-            for (int j = 1; j < 16; ++j) c[j] = bcnt_acc(x[j], c[j]);
+            for (int j = 1; j < 16; ++j) c[j] = kAsm ? bcnt_acc(x[j], c[j]) : c[j] + __popc(x[j]);
         }
     }
+    // kSplit: the masks only in a wave with a masked lane (a wave-uniform branch around two
+    // copies of the moments: the standalone count kernel, where chunk starts are 1 in 1,024
+    // blocks at the reference's chunk length), and the accumulating v_bcnt; otherwise always
+    // masked and the compiler's popcounts (the E-step's fused counts: inside its 128-VGPR
+    // budget the inline-asm popcounts cost 6 spills)
+    template <bool kSplit = true>
     __device__ __forceinline__ void block(uint4 w, uint2 s, uint32_t wprev, uint32_t sprev,
                                           bool cstart, uint32_t* lds, bool valid = true) {
         if (cstart) sprev = 0u;
         const uint32_t vm = valid ? ~0u : 0u;
         const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
-        // no transition into a chunk's position 0, nothing from a lane without a block: the
-        // masks only in a wave with such a lane (a wave-uniform branch; chunk starts are 1 in
-        // 1,024 blocks at the reference's chunk length)
-        if (__builtin_amdgcn_ballot_w64(cstart || !valid))
-            moments<true>(ww, wprev, cstart ? (vm & ~1u) : vm, vm);
+        // no transition into a chunk's position 0, nothing from a lane without a block
+        if (!kSplit || __builtin_amdgcn_ballot_w64(cstart || !valid))
+            moments<true, kSplit>(ww, wprev, cstart ? (vm & ~1u) : vm, vm);
         else
-            moments<false>(ww, wprev, ~0u, ~0u);
+            moments<false, kSplit>(ww, wprev, ~0u, ~0u);
         c[0] += valid ? (cstart ? 63u : 64u) : 0u;
         // the '+' work (rare: island blocks)
         const bool plus = valid && (s.x | s.y | sprev) != 0u;

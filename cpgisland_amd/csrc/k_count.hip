@@ -27,6 +27,9 @@ constexpr int kCntRep = cnt::kRep;
 // the grid cap: 4 waves per SIMD (<= 128 VGPRs) hold 1,024 workgroups of 4 waves at once;
 // every lane has two rounds in flight (the one being counted and the next one's loads)
 constexpr int kCntGrid = 2048;
+// s_waitcnt vmcnt(0) (gfx9 encoding: vmcnt 0, expcnt 7, lgkmcnt 15 — only the vector memory
+// counter is waited for)
+constexpr int kVmcnt0 = 0x0F70;
 constexpr int kCntWavesPerEU = 4;
 
 // the value of `v` in the lane below (wave_shr:1 DPP); lane 0 takes `old`
@@ -93,17 +96,23 @@ void k_count_main(const uint4* __restrict__ packed4, const uint2* __restrict__ s
     };
     uint32_t zv;
     asm volatile("v_mov_b32 %0, 0" : "=v"(zv));
-    // full rounds, two per iteration: the next round's loads are issued before the current one
-    // is counted (ping-pong buffers); a round is full when the wave's last block of it lies
-    // before the end (wave-uniform)
+    // full rounds, two per iteration (ping-pong buffers): the next round's loads are issued
+    // before the current one is counted — and only once the current round's have landed
+    // (vmcnt(0)), so that a wave holds exactly ONE round of loads in flight while it counts,
+    // never two: on this chip a streaming read runs faster with fewer requests outstanding
+    // (tools/loadshape.hip: one round in flight per wave 6.1-6.5 TB/s, two 5.4-5.8; the count
+    // kernel 0.2435-0.2538 -> 0.2314-0.2330 ms at 3.1 Gbp, profiles/r06_count/).  A round is
+    // full when the wave's last block of it lies before the end (wave-uniform).
     const int64_t gfull = nblk - 64;
     Round A, B;
     if (g <= gfull) load_round(A, packed4, sign2, packed, sign, g, lane, zv);
     while (g <= gfull) {
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);
         if (g + step <= gfull) load_round(B, packed4, sign2, packed, sign, g + step, lane, zv);
         count_round(A, g, true);
         g += step;
         if (g > gfull) break;
+        __builtin_amdgcn_s_waitcnt(kVmcnt0);
         if (g + step <= gfull) load_round(A, packed4, sign2, packed, sign, g + step, lane, zv);
         count_round(B, g, true);
         g += step;

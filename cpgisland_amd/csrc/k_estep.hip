@@ -367,7 +367,7 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
         __builtin_amdgcn_sched_barrier(0);   // kept apart from phase 1: registers
         if (t == 0) atomicAdd(&scnt[64 + cnt::init_state(cd0.raw[0], sg.x)], 1u);
         cnt::Lane lc;
-        lc.block(make_uint4(cd0.raw[0], cd0.raw[1], cd0.raw[2], cd0.raw[3]), sg, cd0.prev,
+        lc.template block<false>(make_uint4(cd0.raw[0], cd0.raw[1], cd0.raw[2], cd0.raw[3]), sg, cd0.prev,
                  sgp >> 31, t == 0, scnt);
         lc.flush(scnt);
         __builtin_amdgcn_sched_barrier(0);
@@ -518,7 +518,7 @@ __device__ __forceinline__ void estep_chunk(const cpg_model& model, const uint32
             const uint2 sw = *reinterpret_cast<const uint2*>(sk + 2 * t);
             const uint32_t swp = sk[2 * t - 1];
             cnt::Lane lc;
-            lc.block(w, sw, wp, swp >> 31, false, scnt);
+            lc.template block<false>(w, sw, wp, swp >> 31, false, scnt);
             lc.flush(scnt);
         }
     }

@@ -1478,7 +1478,19 @@ __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
     //    cost one memory latency on this one-workgroup-per-chunk critical path)
     __shared__ C64 sPre[kMaxStagedBar], sPost[kMaxStagedBar];
     __shared__ int sPt[kMaxStagedBar];
+    // the staged barriers' blocks: their 16 packed words and the word before, loaded in this
+    // same round as the plans (the window codes of phase C come from here, not from a third
+    // dependent round trip to memory)
+    __shared__ uint32_t sWd[kMaxStagedBar * 17];
     C64* sRx = sGap;   // rx of barrier i, replaced by its gap composite
+    {
+        const int nstb = min(nbar, kMaxStagedBar);
+        for (int w = t; w < nstb * 17; w += kSegT) {
+            const int bi = w / 17, j = w - bi * 17;
+            const int64_t wi = (int64_t)sBar[bi] * kSBWords - 1 + j;
+            sWd[w] = wi >= 0 ? pk[wi] : 0u;
+        }
+    }
     for (int i = t; i < nbar; i += kSegT) {
         const int k = sBar[i];
         blc[i] = k;
@@ -1556,10 +1568,12 @@ __global__ __launch_bounds__(kSegT) void k_vit_chain_seg(
         const int off = sWoff[i];
         const int len = max(0, sWb[i] - sWa[i]);
         if (off + len > kStageSteps) continue;
+        const uint32_t* wd = sWd + i * 17 + 1;   // word q of block sWk[i] at wd[q], q >= -1
         for (int j = t & 63; j < len; j += 64) {
-            const int64_t pos = sWk[i] * kSB + sWa[i] + j;
-            const uint32_t d = base_at(pk, pos - 1) | (base_at(pk, pos) << 2);
-            stageL[off + j] = sL[d];
+            const int q = sWa[i] + j;              // position within the block (q - 1 >= -1)
+            const uint32_t b1 = (wd[q >> 4] >> ((q & 15) * 2)) & 3u;
+            const uint32_t b0 = (wd[(q - 1) >> 4] >> (((q - 1) & 15) * 2)) & 3u;
+            stageL[off + j] = sL[b0 | (b1 << 2)];
         }
     }
     __syncthreads();

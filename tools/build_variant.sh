@@ -1,7 +1,7 @@
 #!/bin/bash
 # build/abl/libcpg_<name>.so from a PATCHED copy of the sources (development measurement only;
 # the product sources carry no build-time knobs):
-#   tools/build_variant.sh <name> "<extra flags>" ['<file>:<sed expression>' ...]
+#   tools/build_variant.sh <name> "<extra flags>" ['<file>:<sed expression>' | '<file>:@<script.py>' ...]
 # e.g. tools/build_variant.sh grid4k "" 'k_count.hip:s/kCntGrid = 2048/kCntGrid = 4096/'
 # Every expression must change its file (checked), so a stale patch fails loudly.
 set -e
@@ -16,7 +16,8 @@ cp $ROOT/include/cpg.h $SRC/include/
 for p in "$@"; do
   f=${p%%:*}; e=${p#*:}
   cp $SRC/csrc/$f $SRC/csrc/$f.orig
-  sed -i -e "$e" $SRC/csrc/$f
+  # '<file>:@<script.py>': the script rewrites the file in place (multi-line edits)
+  if [ "${e:0:1}" = "@" ]; then python3 ${e:1} $SRC/csrc/$f; else sed -i -e "$e" $SRC/csrc/$f; fi
   if cmp -s $SRC/csrc/$f $SRC/csrc/$f.orig; then echo "patch changed nothing: $p" >&2; exit 1; fi
   rm $SRC/csrc/$f.orig
 done
