@@ -579,8 +579,6 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
     shared = bool(dist) and torch.cuda.device_count() < world
     ntr = []   # (start, end) timing events of the training pass, every 4th timed step
 
-    # the decode model: one Baum-Welch iteration over the whole genome from the reference's
-    # model (every rank's E-step merged in rank order), before timing
     def halo_into(b):
         if world == 1:
             return
@@ -597,6 +595,9 @@ def run_c3(args, world, rank, local, dist, backend, dev, emit=True):
     for b in range(2):
         halo_into(b)
     torch.cuda.synchronize()
+    # the decode model: one Baum-Welch iteration over the whole genome from the reference's
+    # model — the oracle's, committed with its whole-genome results (every rank the same);
+    # for other genome sizes the GPU E-step of every rank merged in rank order, before timing
     fx = oracle_fixture("C3", C3_SEED, 0, G)
 
     def gpu_model1():

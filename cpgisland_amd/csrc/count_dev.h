@@ -75,14 +75,14 @@ __device__ __forceinline__ uint32_t compact16(uint32_t x) {
 // common block — no '+' state — adds each popcount straight into its register.
 struct Lane {
     uint32_t c[16];
-    // pprep != nullptr: the '+'->'+' moments go to 16 x 16 lane-spread LDS replicas
-    // (pprep[moment * 16 + lane % 16]; the caller sums them: pp_replicas_sum) by the lanes
-    // that have '+' states; nullptr: the whole wave runs the '+' work when one lane needs it
-    // and adds one wave sum per moment to lds[16 .. 32)
-    uint32_t* pprep;
-    __device__ __forceinline__ explicit Lane(uint32_t* pp_replicas = nullptr) : pprep(pp_replicas) {
+    // the '+'->'+' moments: in the standalone count kernel (kSplit below) per-lane registers
+    // too, added by the lanes that have '+' states and flushed once (flush_plus); in the
+    // E-step's fused counts the whole wave runs the '+' work when one lane needs it and adds one
+    // wave sum per moment to lds[16 .. 32) (registers there are the E-step's)
+    uint32_t cp[16];
+    __device__ __forceinline__ Lane() {
 #pragma unroll
-        for (int d = 0; d < 16; ++d) c[d] = 0u;
+        for (int d = 0; d < 16; ++d) c[d] = cp[d] = 0u;
     }
     // w: the block's 4 packed words; s: its 2 sign words; wprev / sprev: the packed word and
     // the sign bit before the block (ignored at a chunk start: no transition into position 0);
@@ -136,14 +136,16 @@ struct Lane {
         c[0] += valid ? (cstart ? 63u : 64u) : 0u;
         // the '+' work (rare: island blocks)
         const bool plus = valid && (s.x | s.y | sprev) != 0u;
-        if (pprep) {
-            if (plus) plus_block(w, s, wprev, sprev, cstart, lds);
+        if constexpr (kSplit) {
+            if (plus) plus_block<true>(w, s, wprev, sprev, cstart, lds);
         } else if (__builtin_amdgcn_ballot_w64(plus)) {
-            plus_block(w, plus ? s : make_uint2(0u, 0u), wprev, plus ? sprev : 0u, cstart, lds);
+            plus_block<false>(w, plus ? s : make_uint2(0u, 0u), wprev, plus ? sprev : 0u, cstart,
+                              lds);
         }
     }
-    // the '+'->'+' moments (the same planes masked by the '+'->'+' positions) and the sign
-    // changes, straight to LDS
+    // the '+'->'+' moments (the same planes masked by the '+'->'+' positions: kReg into cp[],
+    // else one wave sum per moment to LDS) and the sign changes, straight to LDS
+    template <bool kReg>
     __device__ __forceinline__ void plus_block(uint4 w, uint2 s, uint32_t wprev,
                                                uint32_t sprev, bool cstart, uint32_t* lds) {
         const uint32_t ww[4] = {w.x, w.y, w.z, w.w};
@@ -185,13 +187,9 @@ struct Lane {
             if (j & 8) x &= phi[pr];
             return x;
         };
-        if (pprep) {   // lane-spread replicas [moment][lane % 16]: plain per-lane LDS atomics
-            const int col = threadIdx.x & 15;
+        if constexpr (kReg) {   // per-lane registers (two accumulating v_bcnt per moment)
 #pragma unroll
-            for (int j = 0; j < 16; ++j) {
-                const uint32_t v = __popc(mom(0, j)) + __popc(mom(1, j));
-                if (v) atomicAdd(&pprep[j * 16 + col], v);
-            }
+            for (int j = 0; j < 16; ++j) cp[j] = bcnt_acc(mom(1, j), bcnt_acc(mom(0, j), cp[j]));
         } else {       // the whole wave is here: one reduction, one atomic per moment
             uint32_t m[16];
 #pragma unroll
@@ -219,6 +217,12 @@ struct Lane {
 #pragma unroll
         for (int d = 0; d < 16; ++d) c[d] = 0u;
     }
+    // the '+'->'+' moment registers (the standalone count kernel) -> lds[16 .. 32)
+    __device__ __forceinline__ void flush_plus(uint32_t* lds) {
+        wave_sum16(cp, lds + 16);
+#pragma unroll
+        for (int d = 0; d < 16; ++d) cp[d] = 0u;
+    }
     // lds[0 .. 16) += the wave's sums of c[0 .. 16) (c is clobbered).  Recursive halving (after
     // 4 levels lane L holds sum L & 15 of its 16-lane row, 15 shuffles instead of 16 x 4), then
     // the rows; one LDS atomic per sum (a per-lane atomic on a shared address would become the
@@ -244,17 +248,6 @@ struct Lane {
         if (lane < 16 && x) atomicAdd(&lds[lane], x);
     }
 };
-
-// lds[16 .. 32) += the lane-spread '+'->'+' replicas (Lane::pprep), threads t < 16, after a
-// workgroup barrier
-__device__ __forceinline__ void pp_replicas_sum(const uint32_t* pprep, uint32_t* lds, int t) {
-    if (t < 16) {
-        uint32_t v = 0u;
-#pragma unroll
-        for (int i = 0; i < 16; ++i) v += pprep[t * 16 + ((i + t) & 15)];   // rotated: no conflicts
-        lds[16 + t] += v;
-    }
-}
 
 // raw sum i (< kRaw, the accumulators' layout tot[16] pp[16] pm[16] mp[16] init[8]) from a
 // workgroup's LDS counters: tot and pp from their moments (Lane) by Moebius inversion — the

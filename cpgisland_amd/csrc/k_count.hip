@@ -71,14 +71,12 @@ void k_count_main(const uint4* __restrict__ packed4, const uint2* __restrict__ s
                   int64_t nblk, int64_t blk_per_chunk, unsigned long long* __restrict__ gacc,
                   unsigned int* done, int64_t* __restrict__ out) {
     __shared__ uint32_t scnt[kRaw];   // the workgroup's counters (LDS atomics)
-    __shared__ uint32_t spp[16 * 16];  // '+'->'+' moments, lane-spread replicas (Lane)
     __shared__ uint64_t raw[kRaw];
     __shared__ int s_last;
     const int t = threadIdx.x, lane = t & 63;
     if (t < kRaw) scnt[t] = 0u;
-    spp[t] = 0u;   // (kCountThreads == 256 == 16 x 16)
     __syncthreads();
-    cnt::Lane lc(spp);
+    cnt::Lane lc;
     const int64_t step = (int64_t)gridDim.x * blockDim.x;   // blocks per grid round
     // the wave's first block (wave-uniform): every lane of a wave runs every round, so the
     // flush's shuffles see the whole wave
@@ -131,8 +129,7 @@ void k_count_main(const uint4* __restrict__ packed4, const uint2* __restrict__ s
         count_round(r, g, valid);
     }
     lc.flush(scnt);   // (32-bit counters: a lane's blocks are far below their range)
-    __syncthreads();
-    cnt::pp_replicas_sum(spp, scnt, t);
+    lc.flush_plus(scnt);
     __syncthreads();
     if (t < kRaw) {
         const uint32_t v = cnt::raw_of(scnt, t);

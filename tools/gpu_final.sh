@@ -12,6 +12,8 @@ import json
 a = json.load(open("$OUT/c3_gloo2.json")); b = json.load(open("$OUT/bench_driver.json"))["c3_single_gpu"]
 print("gloo2", a["n_gpus"], round(a["value"] / 1e9, 1), a["fingerprint"])
 print("n1   ", b["fingerprint"])
-print("fingerprints equal:", a["fingerprint"] == b["fingerprint"])
+keys = ("records_sha256", "counts_sha256", "islands", "oracle_match")
+print("fingerprints equal:", all(a["fingerprint"][k] == b["fingerprint"][k] for k in keys),
+      "oracle_match:", a["fingerprint"]["oracle_match"], b["fingerprint"]["oracle_match"])
 print("bw", a["bw_iteration"]["ms_per_iteration"], b["bw_iteration"]["ms_per_iteration"])
 PY
