@@ -852,10 +852,12 @@ def main():
                     help="join both streams after every step (by default step k+1's training "
                          "pass may start while step k's decode still runs: the steps are "
                          "independent batches, pipelined for throughput)")
-    ap.add_argument("--lanes", type=int, default=1,
+    ap.add_argument("--lanes", type=int, default=2,
                     help="pipeline lanes: step k runs on lane k %% lanes, each lane with its own "
                          "context (workspace), stream pair and outputs, so consecutive steps' "
-                         "kernels of the same kind may run concurrently")
+                         "kernels of the same kind may run concurrently (default 2: since the "
+                         "decode has no cross-workgroup waits, two steps' decodes and training "
+                         "passes overlap; 1, 3, 4 measured slower, DESIGN.md 5)")
     ap.add_argument("--decode-lanes", type=int, default=1,
                     help="decodes of consecutive steps alternate over this many contexts, "
                          "streams and output buffers, so that two steps' per-chunk kernels may "
@@ -867,9 +869,10 @@ def main():
     ap.add_argument("--train-cus", type=int, default=-1,
                     help="run the training pass on this many compute units only (a CU-masked "
                          "stream, the first bits of the mask), leaving the rest to the decode; "
-                         "0 = all, -1 = 12/16 of them (default; round 3's two-position E-step, "
-                         "400 steps: 160: 295, 176: 299, 184: 302, 192: 334-348, 200: 330, "
-                         "208: 325-328, 224: 324-325, 240: 309-310 Gbase/s)")
+                         "0 = all, -1 = 14/16 of them (default; round 6, two pipeline lanes, "
+                         "200 steps: 160: 366, 192: 397-401, 208: 402-404, 216: 413, "
+                         "224: 419-427, 232: 422-423, 240: 418-419, 248: 415-416, all 256: "
+                         "393-395 Gbase/s; one lane (rounds 3-5) peaked at 192 = 12/16)")
     ap.add_argument("--decode-cus-from", type=int, default=0,
                     help="> 0: the decode stream CU-masked to compute units [this, all) (a masked "
                          "stream has no priority: the decode then runs at normal priority)")
@@ -1019,7 +1022,7 @@ def main():
     main_s = torch.cuda.current_stream()
     ncu = torch.cuda.get_device_properties(dev).multi_processor_count
     if args.train_cus < 0:
-        args.train_cus = ncu * 12 // 16
+        args.train_cus = ncu * 14 // 16
     if args.train_cus and args.train_cus < ncu and not args.serial:
         if args.train_cu_stride:
             tr_cus = [i for i in range(ncu) if i % args.train_cu_stride != 0][:args.train_cus]
@@ -1297,6 +1300,11 @@ def main():
             roof["traffic_source"] = ("stored PMC profile, not this run: " + pmc["source"])
         # "bound" names the roof the kernel is priced against (the contract's HBM roofline);
         # what actually limits it is measured by the PMC passes and reported beside it
+        # with pipeline lanes, launches of consecutive steps overlap: `achieved` is per launch
+        # (its own duration, shared GPU), the kernel's delivered rate over the timed region is
+        # one launch's algorithmic bytes per step time
+        roof["concurrent_launches"] = nlanes
+        roof["aggregate_achieved"] = round(alg_bytes / (ms_per_step / 1e3) / 1e9, 1)
         roof["limiter"] = "fp64 VALU issue + dependency latency, not HBM (PMC: profiles/*pmc*)"
         roof["note"] = ("exact fp64 forward-backward: ~50 VALU instructions per base against "
                         "0.25 B/base of HBM traffic; DESIGN.md 5")
