@@ -34,9 +34,15 @@ struct HostPin {
 };
 
 // page-lock a caller buffer for the call's duration (DMA straight from it) unless it already
-// is pinned; a failed registration leaves pageable copies (HIP stages them, slower)
+// is pinned; a failed registration leaves pageable copies (HIP stages them, slower).  Buffers
+// under kPinMin stay pageable: staging costs little at that size, and a small caller
+// buffer registered and unregistered here is soon handed out again by the caller's allocator
+// for other (pageable) transfers.  (The one GPU fault seen in the streamed-genome tests,
+// round 6: an illegal address reported in a torch H2D copy right after a 700,000-base call
+// whose 175 KB and 88 KB inputs had been registered here; not reproduced, cause unproven.)
+constexpr size_t kPinMin = 8u << 20;
 void pin_host(HostPin& h, const void* p, size_t bytes) {
-    if (!p || !bytes) return;
+    if (!p || bytes < kPinMin) return;
     hipPointerAttribute_t a;
     if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type == hipMemoryTypeHost) return;
     (void)hipGetLastError();
